@@ -1,0 +1,145 @@
+// Fp2 = Fp[i] / (i^2 + 1): the field of G2 coordinates and of the tower base.
+#pragma once
+#include "fp.h"
+
+namespace bgv {
+
+BGV_HD fp2_t fp2_zero() { fp2_t r; fp_set_zero(r.c0); fp_set_zero(r.c1); return r; }
+BGV_HD fp2_t fp2_one() { fp2_t r; r.c0 = FP_ONE; fp_set_zero(r.c1); return r; }
+
+BGV_HD bool fp2_is_zero(const fp2_t& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+BGV_HD bool fp2_eq(const fp2_t& a, const fp2_t& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
+BGV_HD bool fp2_is_one(const fp2_t& a) { return fp_eq(a.c0, FP_ONE) && fp_is_zero(a.c1); }
+
+BGV_HD void fp2_select(fp2_t& r, bool c, const fp2_t& a, const fp2_t& b) {
+  fp_select(r.c0, c, a.c0, b.c0);
+  fp_select(r.c1, c, a.c1, b.c1);
+}
+
+BGV_HD void fp2_add(fp2_t& r, const fp2_t& a, const fp2_t& b) { fp_add(r.c0, a.c0, b.c0); fp_add(r.c1, a.c1, b.c1); }
+BGV_HD void fp2_sub(fp2_t& r, const fp2_t& a, const fp2_t& b) { fp_sub(r.c0, a.c0, b.c0); fp_sub(r.c1, a.c1, b.c1); }
+BGV_HD void fp2_dbl(fp2_t& r, const fp2_t& a) { fp_dbl(r.c0, a.c0); fp_dbl(r.c1, a.c1); }
+BGV_HD void fp2_neg(fp2_t& r, const fp2_t& a) { fp_neg(r.c0, a.c0); fp_neg(r.c1, a.c1); }
+BGV_HD void fp2_conj(fp2_t& r, const fp2_t& a) { r.c0 = a.c0; fp_neg(r.c1, a.c1); }
+BGV_HD void fp2_mul3(fp2_t& r, const fp2_t& a) { fp_mul3(r.c0, a.c0); fp_mul3(r.c1, a.c1); }
+BGV_HD void fp2_mul4(fp2_t& r, const fp2_t& a) { fp_mul4(r.c0, a.c0); fp_mul4(r.c1, a.c1); }
+BGV_HD void fp2_mul8(fp2_t& r, const fp2_t& a) { fp_mul8(r.c0, a.c0); fp_mul8(r.c1, a.c1); }
+
+// Karatsuba: 3 Fp products
+BGV_HD void fp2_mul(fp2_t& r, const fp2_t& a, const fp2_t& b) {
+  fp_t t0, t1, t2, t3;
+  fp_mul(t0, a.c0, b.c0);
+  fp_mul(t1, a.c1, b.c1);
+  fp_add(t2, a.c0, a.c1);
+  fp_add(t3, b.c0, b.c1);
+  fp_mul(t2, t2, t3);
+  fp_sub(r.c0, t0, t1);
+  fp_sub(t2, t2, t0);
+  fp_sub(r.c1, t2, t1);
+}
+
+// complex squaring: 2 Fp products
+BGV_HD void fp2_sqr(fp2_t& r, const fp2_t& a) {
+  fp_t t0, t1, t2;
+  fp_add(t0, a.c0, a.c1);
+  fp_sub(t1, a.c0, a.c1);
+  fp_mul(t2, a.c0, a.c1);
+  fp_mul(r.c0, t0, t1);
+  fp_dbl(r.c1, t2);
+}
+
+BGV_HD void fp2_mul_fp(fp2_t& r, const fp2_t& a, const fp_t& b) { fp_mul(r.c0, a.c0, b); fp_mul(r.c1, a.c1, b); }
+
+// multiply by the tower non-residue xi = 1 + i
+BGV_HD void fp2_mul_xi(fp2_t& r, const fp2_t& a) {
+  fp_t t0, t1;
+  fp_sub(t0, a.c0, a.c1);
+  fp_add(t1, a.c0, a.c1);
+  r.c0 = t0;
+  r.c1 = t1;
+}
+
+// norm a0^2 + a1^2 in Fp
+BGV_HD void fp2_norm(fp_t& r, const fp2_t& a) {
+  fp_t t0, t1;
+  fp_sqr(t0, a.c0);
+  fp_sqr(t1, a.c1);
+  fp_add(r, t0, t1);
+}
+
+BGV_HD void fp2_inv(fp2_t& r, const fp2_t& a) {
+  fp_t n, t;
+  fp2_norm(n, a);
+  fp_inv(n, n);
+  fp_mul(r.c0, a.c0, n);
+  fp_mul(t, a.c1, n);
+  fp_neg(r.c1, t);
+}
+
+// RFC 9380 sgn0 for Fp2
+BGV_HD uint32_t fp2_sgn0(const fp2_t& a) {
+  const uint32_t s0 = fp_parity(a.c0);
+  const uint32_t z0 = fp_is_zero(a.c0) ? 1u : 0u;
+  const uint32_t s1 = fp_parity(a.c1);
+  return s0 | (z0 & s1);
+}
+
+// ZCash serialization sign: c1 decides unless zero, then c0
+BGV_HD bool fp2_lex_largest(const fp2_t& a) {
+  if (!fp_is_zero(a.c1)) return fp_lex_largest(a.c1);
+  return fp_lex_largest(a.c0);
+}
+
+// Square root in Fp2 through two Fp exponentiations (p = 3 mod 4):
+//   d = sqrt(a0^2 + a1^2)            (exists iff a is a square in Fp2)
+//   t = (a0 + d) / 2,  s = t^((p-3)/4)
+//   s^2 t == 1 :  x = s t + (a1 s / 2) i
+//   otherwise  :  x = (a1 s / 2) - (s t) i      (then -t is the square)
+// a1 == 0 is handled directly in Fp.  Returns false iff a is a non-square.
+BGV_HD bool fp2_sqrt(fp2_t& r, const fp2_t& a) {
+  if (fp_is_zero(a.c1)) {
+    fp_t s;
+    if (fp_sqrt(s, a.c0)) {
+      r.c0 = s;
+      fp_set_zero(r.c1);
+      return true;
+    }
+    fp_t na;
+    fp_neg(na, a.c0);
+    // -1 is a non-residue, so -a0 is a square here: x = sqrt(-a0) * i
+    fp_sqrt(s, na);
+    fp_set_zero(r.c0);
+    r.c1 = s;
+    return true;
+  }
+  fp_t n, d;
+  fp2_norm(n, a);
+  if (!fp_sqrt(d, n)) return false;
+  fp_t t, s, st, s2t, as;
+  fp_add(t, a.c0, d);
+  fp_half(t, t);
+  fp_pow(s, t, EXP_P_MINUS_3_DIV_4);
+  fp_mul(st, s, t);
+  fp_mul(s2t, st, s);
+  fp_mul(as, a.c1, s);
+  fp_half(as, as);
+  if (fp_eq(s2t, FP_ONE)) {
+    r.c0 = st;
+    r.c1 = as;
+  } else {
+    r.c0 = as;
+    fp_neg(r.c1, st);
+  }
+  return true;
+}
+
+// a is a square in Fp2 iff its norm is a square in Fp
+BGV_HD bool fp2_is_square(const fp2_t& a) {
+  fp_t n, l;
+  fp2_norm(n, a);
+  if (fp_is_zero(n)) return true;
+  fp_pow(l, n, EXP_P_MINUS_1_DIV_2);
+  return fp_eq(l, FP_ONE);
+}
+
+}  // namespace bgv

@@ -1,0 +1,113 @@
+// Optimal-ate Miller loop for BLS12-381 (loop over |x| = 0xd201000000010000).
+// Q in G2 is walked in homogeneous projective coordinates on the M-type
+// twist; each line is evaluated at P in G1 (affine) as the sparse element
+//   l = a0 + a1 w^2 + b1 w^3
+// (line scaled by Fp2 factors / w^3, all of which die in the final
+// exponentiation).  Re-creates blst's miller_loop_n used by
+// Pairing::commit/finalverify (packages/beacon-node/src/chain/bls/maybeBatch.ts:18).
+#pragma once
+#include "h2c.h"
+
+namespace bgv {
+
+struct g2p_t { fp2_t x, y, z; };  // homogeneous projective: x = X/Z, y = Y/Z
+
+// T <- 2T, line tangent at T evaluated at P
+BGV_HD void miller_dbl_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const fp_t& xp, const fp_t& yp) {
+  fp2_t A, B, C, E, F, G, H, t;
+  fp2_mul(A, T.x, T.y);
+  fp_half(A.c0, A.c0);
+  fp_half(A.c1, A.c1);           // A = XY/2
+  fp2_sqr(B, T.y);               // Y^2
+  fp2_sqr(C, T.z);               // Z^2
+  fp2_mul(E, C, B2_X3_MONT);     // 3b' Z^2
+  fp2_mul3(F, E);                // 9b' Z^2
+  fp2_add(t, T.y, T.z);
+  fp2_sqr(t, t);
+  fp2_add(H, B, C);
+  fp2_sub(H, t, H);              // 2YZ
+  // line (negated overall): (3b'Z^2 - Y^2) + 3X^2 xP w^2 - 2YZ yP w^3
+  fp2_sub(a0, E, B);
+  fp2_sqr(t, T.x);
+  fp2_mul3(t, t);
+  fp2_mul_fp(a1, t, xp);
+  fp2_mul_fp(t, H, yp);
+  fp2_neg(b1, t);
+  // point
+  fp2_sub(t, B, F);
+  fp2_mul(T.x, A, t);            // X3 = XY/2 (Y^2 - 9b'Z^2)
+  fp2_add(G, B, F);
+  fp_half(G.c0, G.c0);
+  fp_half(G.c1, G.c1);           // (Y^2 + 9b'Z^2)/2
+  fp2_sqr(G, G);
+  fp2_sqr(t, E);
+  fp2_mul3(t, t);                // 27 b'^2 Z^4
+  fp2_sub(T.y, G, t);
+  fp2_mul(T.z, B, H);            // Z3 = 2 Y^3 Z
+}
+
+// T <- T + Q (Q affine), line through T and Q evaluated at P
+BGV_HD void miller_add_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const g2a& Q, const fp_t& xp,
+                            const fp_t& yp) {
+  fp2_t th, la, C, D, E, F, G, H, t;
+  fp2_mul(t, Q.y, T.z);
+  fp2_sub(th, T.y, t);           // theta = Y - yQ Z
+  fp2_mul(t, Q.x, T.z);
+  fp2_sub(la, T.x, t);           // lambda = X - xQ Z
+  // line: (theta xQ - lambda yQ) - theta xP w^2 + lambda yP w^3
+  fp2_mul(a0, th, Q.x);
+  fp2_mul(t, la, Q.y);
+  fp2_sub(a0, a0, t);
+  fp2_mul_fp(t, th, xp);
+  fp2_neg(a1, t);
+  fp2_mul_fp(b1, la, yp);
+  // point
+  fp2_sqr(C, th);
+  fp2_sqr(D, la);
+  fp2_mul(E, D, la);
+  fp2_mul(F, T.z, C);
+  fp2_mul(G, T.x, D);
+  fp2_add(H, E, F);
+  fp2_sub(H, H, G);
+  fp2_sub(H, H, G);
+  fp2_mul(T.x, la, H);
+  fp2_sub(t, G, H);
+  fp2_mul(t, th, t);
+  fp2_mul(C, T.y, E);
+  fp2_sub(T.y, t, C);
+  fp2_mul(T.z, T.z, E);
+}
+
+// f = f_{x, Q}(P) for the negative x (conjugated), P affine in G1, Q affine in G2.
+// P or Q at infinity gives 1.
+BGV_HD void miller_loop(fp12_t& f, const g1a& P, bool p_inf, const g2a& Q, bool q_inf) {
+  fp12_one(f);
+  if (p_inf || q_inf) return;
+  g2p_t T;
+  T.x = Q.x;
+  T.y = Q.y;
+  T.z = fp2_one();
+  fp2_t a0, a1, b1;
+  bool first = true;
+  for (int b = 62; b >= 0; b--) {
+    if (!first) fp12_sqr(f, f);
+    miller_dbl_step(T, a0, a1, b1, P.x, P.y);
+    if (first) {
+      // f = 1 * line
+      fp12_one(f);
+      f.c0.c0 = a0;
+      f.c0.c1 = a1;
+      f.c1.c1 = b1;
+      first = false;
+    } else {
+      fp12_mul_line(f, f, a0, a1, b1);
+    }
+    if ((BLS_X_ABS >> b) & 1ull) {
+      miller_add_step(T, a0, a1, b1, Q, P.x, P.y);
+      fp12_mul_line(f, f, a0, a1, b1);
+    }
+  }
+  fp12_conj(f, f);  // x < 0
+}
+
+}  // namespace bgv

@@ -1,0 +1,105 @@
+// Host-compiled view of the device arithmetic headers (lodestar_amd/csrc/*.h)
+// for CPU-side debugging tests against the Python oracle.  TEST ONLY: the
+// product never executes this; it launches the HIP kernels through libbgv.
+// I/O convention: Fp = 48-byte big-endian plain integer; Fp2 = c0 || c1;
+// affine G2 = x || y (192 B); affine G1 = x || y (96 B); Fp12 = 12 Fp
+// coefficients ordered w^0.c0, w^0.c1, w^1.c0, ... (tower position k at w^k).
+#include <string.h>
+#include "../../lodestar_amd/csrc/pairing.h"
+
+using namespace bgv;
+
+static void get_fp(fp_t& r, const uint8_t* b) { fp_t t; fp_from_be48(t, b); fp_to_mont(r, t); }
+static void put_fp(uint8_t* b, const fp_t& a) { fp_t t; fp_from_mont(t, a); fp_to_be48(b, t); }
+static void get_fp2(fp2_t& r, const uint8_t* b) { get_fp(r.c0, b); get_fp(r.c1, b + 48); }
+static void put_fp2(uint8_t* b, const fp2_t& a) { put_fp(b, a.c0); put_fp(b + 48, a.c1); }
+static void get_g2a(g2a& r, const uint8_t* b) { get_fp2(r.x, b); get_fp2(r.y, b + 96); }
+static void put_g2a(uint8_t* b, const g2a& a) { put_fp2(b, a.x); put_fp2(b + 96, a.y); }
+static void get_g1a(g1a& r, const uint8_t* b) { get_fp(r.x, b); get_fp(r.y, b + 48); }
+static void put_g1a(uint8_t* b, const g1a& a) { put_fp(b, a.x); put_fp(b + 48, a.y); }
+static void put_fp12(uint8_t* b, const fp12_t& f) {
+  const fp2_t* c[6] = {&f.c0.c0, &f.c1.c0, &f.c0.c1, &f.c1.c1, &f.c0.c2, &f.c1.c2};
+  for (int k = 0; k < 6; k++) put_fp2(b + 96 * k, *c[k]);
+}
+static void get_fp12(fp12_t& f, const uint8_t* b) {
+  fp2_t* c[6] = {&f.c0.c0, &f.c1.c0, &f.c0.c1, &f.c1.c1, &f.c0.c2, &f.c1.c2};
+  for (int k = 0; k < 6; k++) get_fp2(*c[k], b + 96 * k);
+}
+// Jacobian -> affine bytes; returns 0 for infinity
+static int put_g2j(uint8_t* b, const g2j& p) { g2a a; bool ok = jac_to_aff(a, p); put_g2a(b, a); return ok; }
+static int put_g1j(uint8_t* b, const g1j& p) { g1a a; bool ok = jac_to_aff(a, p); put_g1a(b, a); return ok; }
+
+extern "C" {
+
+void hc_fp_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { fp_t x, y, z; get_fp(x, a); get_fp(y, b); fp_mul(z, x, y); put_fp(out, z); }
+void hc_fp_add(const uint8_t* a, const uint8_t* b, uint8_t* out) { fp_t x, y, z; get_fp(x, a); get_fp(y, b); fp_add(z, x, y); put_fp(out, z); }
+void hc_fp_sub(const uint8_t* a, const uint8_t* b, uint8_t* out) { fp_t x, y, z; get_fp(x, a); get_fp(y, b); fp_sub(z, x, y); put_fp(out, z); }
+void hc_fp_inv(const uint8_t* a, uint8_t* out) { fp_t x, z; get_fp(x, a); fp_inv(z, x); put_fp(out, z); }
+void hc_fp2_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { fp2_t x, y, z; get_fp2(x, a); get_fp2(y, b); fp2_mul(z, x, y); put_fp2(out, z); }
+void hc_fp2_sqr(const uint8_t* a, uint8_t* out) { fp2_t x, z; get_fp2(x, a); fp2_sqr(z, x); put_fp2(out, z); }
+void hc_fp2_inv(const uint8_t* a, uint8_t* out) { fp2_t x, z; get_fp2(x, a); fp2_inv(z, x); put_fp2(out, z); }
+int hc_fp2_sqrt(const uint8_t* a, uint8_t* out) { fp2_t x, z; get_fp2(x, a); int ok = fp2_sqrt(z, x); put_fp2(out, z); return ok; }
+int hc_fp2_is_square(const uint8_t* a) { fp2_t x; get_fp2(x, a); return fp2_is_square(x); }
+int hc_fp2_sgn0(const uint8_t* a) { fp2_t x; get_fp2(x, a); return (int)fp2_sgn0(x); }
+
+void hc_fp12_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { fp12_t x, y, z; get_fp12(x, a); get_fp12(y, b); fp12_mul(z, x, y); put_fp12(out, z); }
+void hc_fp12_sqr(const uint8_t* a, uint8_t* out) { fp12_t x, z; get_fp12(x, a); fp12_sqr(z, x); put_fp12(out, z); }
+void hc_fp12_inv(const uint8_t* a, uint8_t* out) { fp12_t x, z; get_fp12(x, a); fp12_inv(z, x); put_fp12(out, z); }
+void hc_fp12_frob(const uint8_t* a, int k, uint8_t* out) { fp12_t x, z; get_fp12(x, a); fp12_frob(z, x, k); put_fp12(out, z); }
+void hc_fp12_cyc_sqr(const uint8_t* a, uint8_t* out) { fp12_t x, z; get_fp12(x, a); fp12_cyclotomic_sqr(z, x); put_fp12(out, z); }
+void hc_fp12_final_exp(const uint8_t* a, uint8_t* out) { fp12_t x, z; get_fp12(x, a); fp12_final_exp(z, x); put_fp12(out, z); }
+void hc_fp12_mul_line(const uint8_t* f, const uint8_t* a0, const uint8_t* a1, const uint8_t* b1, uint8_t* out) {
+  fp12_t x, z; fp2_t l0, l1, l2; get_fp12(x, f); get_fp2(l0, a0); get_fp2(l1, a1); get_fp2(l2, b1);
+  fp12_mul_line(z, x, l0, l1, l2); put_fp12(out, z);
+}
+
+int hc_g2_decompress(const uint8_t* in96, uint8_t* out192, int* inf) {
+  g2a a; bool i; int code = g2_decompress(a, i, in96); *inf = i; if (code == 0) put_g2a(out192, a); return code;
+}
+int hc_g2_deserialize(const uint8_t* in192, uint8_t* out192, int* inf) {
+  g2a a; bool i; int code = g2_deserialize(a, i, in192); *inf = i; if (code == 0) put_g2a(out192, a); return code;
+}
+int hc_g1_decompress(const uint8_t* in48, uint8_t* out96, int* inf) {
+  g1a a; bool i; int code = g1_decompress(a, i, in48); *inf = i; if (code == 0) put_g1a(out96, a); return code;
+}
+int hc_g2_in_subgroup(const uint8_t* aff192) { g2a a; get_g2a(a, aff192); g2j j; jac_from_aff(j, a); return g2_in_subgroup(j); }
+int hc_g2_mul_u64(const uint8_t* aff192, uint64_t k, uint8_t* out192) { g2a a; get_g2a(a, aff192); g2j j, r; jac_from_aff(j, a); jac_mul_u64(r, j, k); return put_g2j(out192, r); }
+int hc_g1_mul_u64(const uint8_t* aff96, uint64_t k, uint8_t* out96) { g1a a; get_g1a(a, aff96); g1j j, r; jac_from_aff(j, a); jac_mul_u64(r, j, k); return put_g1j(out96, r); }
+int hc_g2_add(const uint8_t* a192, const uint8_t* b192, uint8_t* out192) {
+  g2a a, b; get_g2a(a, a192); get_g2a(b, b192); g2j ja, jb, r; jac_from_aff(ja, a); jac_from_aff(jb, b); jac_add(r, ja, jb); return put_g2j(out192, r);
+}
+int hc_g2_dbl(const uint8_t* a192, uint8_t* out192) { g2a a; get_g2a(a, a192); g2j ja, r; jac_from_aff(ja, a); jac_dbl(r, ja); return put_g2j(out192, r); }
+int hc_g1_sum(const uint8_t* pts96, int n, uint8_t* out96) {
+  g1j acc; jac_set_inf(acc);
+  for (int i = 0; i < n; i++) { g1a a; get_g1a(a, pts96 + 96 * i); jac_add_aff(acc, acc, a); }
+  return put_g1j(out96, acc);
+}
+int hc_clear_cofactor(const uint8_t* aff192, uint8_t* out192) { g2a a; get_g2a(a, aff192); g2j j, r; jac_from_aff(j, a); g2_clear_cofactor(r, j); return put_g2j(out192, r); }
+
+void hc_expand_message(const uint8_t* msg32, uint8_t* out256) {
+  uint32_t w[64]; expand_message_xmd_256(w, msg32);
+  for (int i = 0; i < 64; i++) { out256[4*i] = w[i] >> 24; out256[4*i+1] = w[i] >> 16; out256[4*i+2] = w[i] >> 8; out256[4*i+3] = w[i]; }
+}
+void hc_hash_to_field(const uint8_t* msg32, uint8_t* out384) { fp2_t u0, u1; hash_to_field_fp2x2(u0, u1, msg32); put_fp2(out384, u0); put_fp2(out384 + 192 - 96, u1); }
+void hc_sswu(const uint8_t* u96, uint8_t* out192) { fp2_t u; get_fp2(u, u96); g2a q; map_to_curve_sswu(q, u); put_g2a(out192, q); }
+int hc_iso_map(const uint8_t* aff192, uint8_t* out192) { g2a a; get_g2a(a, aff192); g2j r; iso_map_g2(r, a); return put_g2j(out192, r); }
+int hc_hash_to_g2(const uint8_t* msg32, uint8_t* out192) { g2j r; hash_to_g2(r, msg32); return put_g2j(out192, r); }
+
+void hc_miller_loop(const uint8_t* p96, const uint8_t* q192, uint8_t* out576) {
+  g1a p; g2a q; get_g1a(p, p96); get_g2a(q, q192); fp12_t f; miller_loop(f, p, false, q, false); put_fp12(out576, f);
+}
+void hc_miller_dbl_step(const uint8_t* t288, const uint8_t* p96, uint8_t* t_out288, uint8_t* line288) {
+  g2p_t T; get_fp2(T.x, t288); get_fp2(T.y, t288 + 96); get_fp2(T.z, t288 + 192);
+  g1a p; get_g1a(p, p96); fp2_t a0, a1, b1;
+  miller_dbl_step(T, a0, a1, b1, p.x, p.y);
+  put_fp2(t_out288, T.x); put_fp2(t_out288 + 96, T.y); put_fp2(t_out288 + 192, T.z);
+  put_fp2(line288, a0); put_fp2(line288 + 96, a1); put_fp2(line288 + 192, b1);
+}
+void hc_miller_add_step(const uint8_t* t288, const uint8_t* q192, const uint8_t* p96, uint8_t* t_out288, uint8_t* line288) {
+  g2p_t T; get_fp2(T.x, t288); get_fp2(T.y, t288 + 96); get_fp2(T.z, t288 + 192);
+  g2a q; get_g2a(q, q192); g1a p; get_g1a(p, p96); fp2_t a0, a1, b1;
+  miller_add_step(T, a0, a1, b1, q, p.x, p.y);
+  put_fp2(t_out288, T.x); put_fp2(t_out288 + 96, T.y); put_fp2(t_out288 + 192, T.z);
+  put_fp2(line288, a0); put_fp2(line288 + 96, a1); put_fp2(line288 + 192, b1);
+}
+}
