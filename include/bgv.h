@@ -1,0 +1,187 @@
+/*
+ * bgv.h -- C ABI of the MI355X (gfx950) BLS12-381 signature-set batch
+ * verifier ("bgv" = BLS GPU verifier).
+ *
+ * This is the drop-in boundary for the hot path of
+ *   IBlsVerifier.verifySignatureSets(sets, opts)
+ *   (packages/beacon-node/src/chain/bls/interface.ts:20-51)
+ * in maschad/lodestar.  Every entry point below names the reference
+ * interface it replaces.  Plain pointers and sizes only; no torch / HIP
+ * types appear in the signatures.  All functions return 0 (BGV_OK) on
+ * success or a negative BGV_E* status; per-set verification outcomes are
+ * reported as the positive blst error codes listed in bgv_set_code.
+ *
+ * Threading: a bgv_ctx owns one HIP device and one stream.  Calls on one
+ * context must be serialised by the caller (the N-API / Python host layers
+ * do this); different contexts may be used from different threads.
+ */
+#ifndef BGV_H
+#define BGV_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BGV_ABI_VERSION 1
+
+/* ---- status of an API call (negative) ---------------------------------- */
+enum bgv_status {
+  BGV_OK = 0,
+  BGV_E_INVALID_ARG = -1,
+  BGV_E_HIP = -2,          /* HIP runtime error (device missing, OOM, fault) */
+  BGV_E_NO_DEVICE = -3,
+  BGV_E_TABLE_RANGE = -4,  /* pubkey index outside the resident table */
+  BGV_E_EMPTY_SET = -5,    /* a set with zero pubkeys (EMPTY_AGGREGATE_ARRAY) */
+};
+
+/* ---- per-set / per-job outcome codes (>= 0) ------------------------------
+ * Numbering follows blst's BLST_ERROR enum (the codes @chainsafe/blst turns
+ * into "BLST_ERROR: BLST_<NAME>" exceptions), plus the size condition
+ * @chainsafe/blst raises before reaching blst and a range guard for
+ * device-resident index lists.                                             */
+enum bgv_set_code {
+  BGV_SET_OK = 0,
+  BGV_SET_BAD_ENCODING = 1,
+  BGV_SET_POINT_NOT_ON_CURVE = 2,
+  BGV_SET_POINT_NOT_IN_GROUP = 3,
+  BGV_SET_AGGR_TYPE_MISMATCH = 4,
+  BGV_SET_VERIFY_FAIL = 5,
+  BGV_SET_PK_IS_INFINITY = 6,
+  BGV_SET_BAD_SCALAR = 7,
+  BGV_SET_INVALID_SIZE = 8,
+  BGV_SET_INDEX_RANGE = 9, /* device batch named a pubkey index >= table size */
+};
+
+/* job verdicts written to job_result[] */
+enum bgv_job_result {
+  BGV_JOB_INVALID = 0, /* encodings fine, pairing check failed -> resolve(false) */
+  BGV_JOB_VALID = 1,   /* every set verified                  -> resolve(true)  */
+  /* negative: -(bgv_set_code) of the first set (in set order) that could not
+   * be parsed / validated -> reject(Error("BLST_ERROR: BLST_<NAME>"))       */
+};
+
+/* pubkey wire formats accepted by bgv_pubkeys_set */
+enum bgv_pk_format {
+  BGV_PK_COMPRESSED_48 = 0,   /* ZCash compressed G1, as in BeaconState.validators */
+  BGV_PK_UNCOMPRESSED_96 = 1, /* x||y big-endian; PointFormat.uncompressed
+                                 (multithread/index.ts:132,177) */
+};
+
+typedef struct bgv_ctx bgv_ctx;
+
+/* One device batch = n_sets signature sets grouped into n_jobs jobs.  A job
+ * is what the reference hands to verifySignatureSetsMaybeBatch
+ * (chain/bls/maybeBatch.ts:16-38): its verdict is the AND of its sets.
+ * Sets of one job are contiguous: job j owns sets [job_offsets[j],
+ * job_offsets[j+1]).
+ *
+ * Pubkeys arrive as index lists into the HBM-resident index2pubkey table
+ * (state-transition/src/cache/pubkeyCache.ts:6) instead of serialized
+ * points: set i aggregates table entries pk_indices[pk_offsets[i] ..
+ * pk_offsets[i+1]).  An index with bit 31 set selects entry
+ * (index & 0x7fffffff) of raw_pks instead (pubkeys not in the table, e.g.
+ * BLS-to-execution changes, signatureSets/blsToExecutionChange.ts:32).
+ *
+ * Signatures: sig_len[i] bytes at sigs + 192*i (96 = compressed,
+ * 192 = uncompressed; any other length yields BGV_SET_INVALID_SIZE, the
+ * reference's "BLST_INVALID_SIZE", e2e/chain/bls/multithread.test.ts:97).
+ *
+ * scalars: 64-bit non-zero random multipliers, one per set (blst
+ * mul_n_aggregate randomness).  NULL = drawn from getrandom() inside the
+ * library (production).  Tests inject them for reproducibility.
+ *
+ * When `on_device` is non-zero every array pointer is a device pointer on
+ * the context's device (inputs already resident in HBM); otherwise they are
+ * host pointers and the library stages them.                             */
+typedef struct bgv_batch {
+  uint32_t n_sets;
+  uint32_t n_jobs;
+  const uint32_t* job_offsets; /* [n_jobs + 1] */
+  const uint32_t* pk_offsets;  /* [n_sets + 1] */
+  const uint32_t* pk_indices;  /* [pk_offsets[n_sets]] */
+  const uint8_t* raw_pks;      /* [n_raw][96] uncompressed big-endian, may be NULL */
+  uint32_t n_raw;
+  const uint8_t* msgs;         /* [n_sets][32] signing roots */
+  const uint8_t* sigs;         /* [n_sets][192] */
+  const uint32_t* sig_len;     /* [n_sets] */
+  const uint64_t* scalars;     /* [n_sets] or NULL */
+  uint32_t on_device;
+} bgv_batch;
+
+/* Timings of the last bgv_verify call (ms, HIP events on the context's
+ * stream) plus the counters the reference pool exports as
+ * lodestar_bls_thread_pool_* metrics (metrics/metrics/lodestar.ts:350-430). */
+#define BGV_N_STAGES 10
+typedef struct bgv_stats {
+  float stage_ms[BGV_N_STAGES]; /* see bgv_stage_name() */
+  float total_ms;
+  uint32_t batch_retries;       /* 1 when the whole-batch check failed */
+  uint32_t batch_sigs_success;  /* sets accepted by the whole-batch check */
+  uint32_t n_sets;
+  uint32_t n_jobs;
+  uint64_t pubkeys_aggregated;  /* lodestar_bls_aggregated_pubkeys_total */
+} bgv_stats;
+
+int bgv_abi_version(void);
+const char* bgv_set_code_name(int code); /* "BLST_BAD_ENCODING", ... */
+const char* bgv_stage_name(int stage);
+const char* bgv_last_error(void);        /* thread-local text of the last failure */
+
+/* Open a context on HIP device `device` (chain/chain.ts:199-202 picks the
+ * verifier at node start; this is the GPU branch's constructor, replacing
+ * `new BlsMultiThreadWorkerPool(opts, modules)`, multithread/index.ts:120). */
+int bgv_open(int device, bgv_ctx** out);
+/* BlsMultiThreadWorkerPool.close (multithread/index.ts:193-214) */
+int bgv_close(bgv_ctx* ctx);
+
+/* index2pubkey table management: mirrors syncPubkeys / addPubkey
+ * (state-transition/src/cache/pubkeyCache.ts:56-77, cache/epochContext.ts:
+ * 701-704).  Keys are trusted (validated at deposit, block/processDeposit.ts:
+ * 57-66) and stored as affine Montgomery (x, y), 96 B per validator.     */
+int bgv_pubkeys_set(bgv_ctx* ctx, uint32_t first_index, uint32_t n, const uint8_t* data, uint32_t format);
+int bgv_pubkeys_count(bgv_ctx* ctx, uint32_t* count);
+/* read back entries as 96-byte uncompressed big-endian (tests, checkpoints) */
+int bgv_pubkeys_get(bgv_ctx* ctx, uint32_t first_index, uint32_t n, uint8_t* out96);
+
+/* Verify one device batch.  Replaces the worker body
+ * verifyManySignatureSets (multithread/worker.ts:30-106) together with
+ * verifySignatureSetsMaybeBatch (maybeBatch.ts:16-38) and the main-thread
+ * aggregation getAggregatedPubkey (chain/bls/utils.ts:5-16):
+ *   job_result[n_jobs]  (host memory) BGV_JOB_* per job;
+ *   set_code[n_sets]    (host memory, may be NULL) bgv_set_code per set;
+ *   stats               (may be NULL).
+ * One whole-batch pairing check runs first; only when it fails is every
+ * job checked on its own (the worker's per-job retry, worker.ts:74-85). */
+int bgv_verify(bgv_ctx* ctx, const bgv_batch* batch, int32_t* job_result, int32_t* set_code, bgv_stats* stats);
+
+/* Multi-GPU partials: run the batch up to, but excluding, the
+ * final exponentiation and return this shard's Miller product (576 B, 12
+ * Fp coefficients of w^0..w^5, c0||c1 each, 48-byte big-endian) with the
+ * per-set codes.  ok_out = 1 when no set failed to parse. */
+int bgv_partial(bgv_ctx* ctx, const bgv_batch* batch, uint8_t* miller576, int32_t* set_code, int32_t* ok_out);
+/* Combine n partial Miller products and run ONE final exponentiation:
+ * *is_one = 1 iff the product maps to 1 in GT. */
+int bgv_combine_final(bgv_ctx* ctx, const uint8_t* millers576, uint32_t n, int32_t* is_one);
+
+/* ---- synthetic workload generation (bench / tests; not on the verify path) */
+/* table[first .. first+n) := sk_i * G1 with sk_i = SHA256("bgv-sk" || LE64(seed)
+ * || LE32(i)) mod r; keeps sk on the device for bgv_gen_sign. */
+int bgv_gen_keys(bgv_ctx* ctx, uint32_t first_index, uint32_t n, uint64_t seed);
+/* sigs96[i] = compress((sum_{j in set i} sk_j mod r) * H(msgs[i])).
+ * Pointers follow batch->on_device; sigs_out is in the same space. */
+int bgv_gen_sign(bgv_ctx* ctx, const bgv_batch* batch, uint8_t* sigs_out192);
+
+/* ---- microbenchmarks for the roofline ------------------------ */
+/* Montgomery Fp-mul throughput: `lanes` independent chains of `iters`
+ * products; returns device ms (HIP events). */
+int bgv_bench_fpmul(bgv_ctx* ctx, uint32_t lanes, uint32_t iters, float* ms);
+/* raw v_mad_u64_u32 throughput: lanes * iters * 8 dependent-free mads */
+int bgv_bench_mad(bgv_ctx* ctx, uint32_t lanes, uint32_t iters, float* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BGV_H */

@@ -1,0 +1,497 @@
+// Host side of the C ABI declared in include/bgv.h: context, HBM-resident
+// pubkey table, batch staging and the stage pipeline on one HIP stream.
+//
+// Reference behaviour re-created (packages/beacon-node/src/chain/bls/):
+//   * multithread/worker.ts:30-106  one batch check, per-job fallback
+//   * maybeBatch.ts:16-38           job verdict = AND of its sets; parse
+//                                    errors reject the job
+//   * utils.ts:5-16                 pubkey aggregation (now on the device)
+//   * multithread/index.ts:193-214  close()
+#include <sys/random.h>
+#include <string.h>
+#include <stdio.h>
+#include <stdarg.h>
+#include <vector>
+#include <string>
+
+#include "bgv_internal.h"
+#include "../../include/bgv.h"
+
+using namespace bgv;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(x)                                                                         \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess) return fail(BGV_E_HIP, "%s: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+  } while (0)
+
+template <class T>
+struct dbuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t n) {
+    if (n <= cap) return 0;
+    size_t c = cap ? cap : 64;
+    while (c < n) c *= 2;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc((void**)&p, c * sizeof(T)) != hipSuccess) return fail(BGV_E_HIP, "hipMalloc(%zu) failed", c * sizeof(T));
+    cap = c;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct bgv_ctx {
+  int device = 0;
+  hipStream_t st = nullptr;
+  hipEvent_t ev[ST_COUNT + 1] = {};
+  // index2pubkey table (grown by copy) and synthetic secret keys
+  g1a* table = nullptr;
+  uint32_t table_n = 0, table_cap = 0;
+  dbuf<uint32_t> sk;
+  // staging for host batches
+  dbuf<uint32_t> job_off, pk_off, pk_idx, sig_len;
+  dbuf<uint8_t> raw_in, msgs, sigs, gen_out;
+  dbuf<uint64_t> scalars;
+  dbuf<g1a> raw_conv;
+  // per-batch intermediates
+  dbuf<g2a> sig_aff, h_aff;
+  dbuf<uint32_t> sig_inf, flags;
+  dbuf<int32_t> sig_code, pk_code, job_code, job_result, set_code;
+  dbuf<g1a> rpk_aff;
+  dbuf<g2j> rsig;
+  dbuf<fp12_t> f_set, f_job, f_part;
+  // microbench scratch
+  dbuf<fp_t> mb_fp;
+  dbuf<uint64_t> mb_u64;
+};
+
+// Definitions below take C linkage from their declarations in bgv.h.
+
+int bgv_abi_version(void) { return BGV_ABI_VERSION; }
+const char* bgv_last_error(void) { return g_err.c_str(); }
+
+const char* bgv_set_code_name(int code) {
+  switch (code) {
+    case 0: return "BLST_SUCCESS";
+    case 1: return "BLST_BAD_ENCODING";
+    case 2: return "BLST_POINT_NOT_ON_CURVE";
+    case 3: return "BLST_POINT_NOT_IN_GROUP";
+    case 4: return "BLST_AGGR_TYPE_MISMATCH";
+    case 5: return "BLST_VERIFY_FAIL";
+    case 6: return "BLST_PK_IS_INFINITY";
+    case 7: return "BLST_BAD_SCALAR";
+    case 8: return "BLST_INVALID_SIZE";
+    case 9: return "BGV_INDEX_RANGE";
+    case 10: return "EMPTY_SIGNATURE_SET";
+    default: return "BGV_UNKNOWN";
+  }
+}
+
+const char* bgv_stage_name(int stage) {
+  static const char* names[ST_COUNT] = {"sig_decode_subgroup", "hash_to_g2", "pk_aggregate_scale", "sig_scale",
+                                        "miller_loop",          "job_reduce", "batch_product",      "batch_final_exp",
+                                        "job_final_exp",        "set_codes"};
+  return (stage >= 0 && stage < ST_COUNT) ? names[stage] : "unknown";
+}
+
+int bgv_open(int device, bgv_ctx** out) {
+  if (!out) return fail(BGV_E_INVALID_ARG, "out is NULL");
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(BGV_E_NO_DEVICE, "no HIP device visible");
+  if (device < 0 || device >= n) return fail(BGV_E_NO_DEVICE, "device %d out of range (%d devices)", device, n);
+  HIPCHK(hipSetDevice(device));
+  bgv_ctx* c = new bgv_ctx();
+  c->device = device;
+  HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+  for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+  *out = c;
+  return BGV_OK;
+}
+
+int bgv_close(bgv_ctx* c) {
+  if (!c) return BGV_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->st);
+  for (auto& e : c->ev) (void)hipEventDestroy(e);
+  if (c->table) (void)hipFree(c->table);
+  c->sk.release();
+  c->job_off.release(); c->pk_off.release(); c->pk_idx.release(); c->sig_len.release();
+  c->raw_in.release(); c->msgs.release(); c->sigs.release(); c->gen_out.release();
+  c->scalars.release(); c->raw_conv.release();
+  c->sig_aff.release(); c->h_aff.release(); c->sig_inf.release(); c->flags.release();
+  c->sig_code.release(); c->pk_code.release(); c->job_code.release(); c->job_result.release(); c->set_code.release();
+  c->rpk_aff.release(); c->rsig.release(); c->f_set.release(); c->f_job.release(); c->f_part.release();
+  c->mb_fp.release(); c->mb_u64.release();
+  (void)hipStreamDestroy(c->st);
+  delete c;
+  return BGV_OK;
+}
+
+static int table_reserve(bgv_ctx* c, uint32_t n) {
+  if (n <= c->table_cap) return 0;
+  uint32_t cap = c->table_cap ? c->table_cap : 1024;
+  while (cap < n) cap = cap * 2u > cap ? cap * 2u : n;
+  g1a* t = nullptr;
+  HIPCHK(hipMalloc((void**)&t, (size_t)cap * sizeof(g1a)));
+  HIPCHK(hipMemsetAsync(t, 0, (size_t)cap * sizeof(g1a), c->st));
+  if (c->table) {
+    HIPCHK(hipMemcpyAsync(t, c->table, (size_t)c->table_n * sizeof(g1a), hipMemcpyDeviceToDevice, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    HIPCHK(hipFree(c->table));
+  }
+  c->table = t;
+  c->table_cap = cap;
+  return 0;
+}
+
+int bgv_pubkeys_set(bgv_ctx* c, uint32_t first, uint32_t n, const uint8_t* data, uint32_t fmt) {
+  if (!c || (!data && n)) return fail(BGV_E_INVALID_ARG, "null argument");
+  if (fmt != BGV_PK_COMPRESSED_48 && fmt != BGV_PK_UNCOMPRESSED_96) return fail(BGV_E_INVALID_ARG, "bad format %u", fmt);
+  if (n == 0) return BGV_OK;
+  HIPCHK(hipSetDevice(c->device));
+  if (int r = table_reserve(c, first + n)) return r;
+  const size_t w = fmt == BGV_PK_COMPRESSED_48 ? 48 : 96;
+  if (int r = c->raw_in.ensure((size_t)n * w)) return r;
+  HIPCHK(hipMemcpyAsync(c->raw_in.p, data, (size_t)n * w, hipMemcpyHostToDevice, c->st));
+  if (fmt == BGV_PK_COMPRESSED_48) launch_table_from_compressed(c->st, c->raw_in.p, c->table + first, n);
+  else launch_table_from_uncompressed(c->st, c->raw_in.p, c->table + first, n);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->st));
+  if (first + n > c->table_n) c->table_n = first + n;
+  return BGV_OK;
+}
+
+int bgv_pubkeys_count(bgv_ctx* c, uint32_t* count) {
+  if (!c || !count) return fail(BGV_E_INVALID_ARG, "null argument");
+  *count = c->table_n;
+  return BGV_OK;
+}
+
+int bgv_pubkeys_get(bgv_ctx* c, uint32_t first, uint32_t n, uint8_t* out96) {
+  if (!c || (!out96 && n)) return fail(BGV_E_INVALID_ARG, "null argument");
+  if ((uint64_t)first + n > c->table_n) return fail(BGV_E_TABLE_RANGE, "range [%u, %u) beyond table size %u", first, first + n, c->table_n);
+  if (n == 0) return BGV_OK;
+  HIPCHK(hipSetDevice(c->device));
+  if (int r = c->gen_out.ensure((size_t)n * 96)) return r;
+  launch_table_export(c->st, c->table + first, c->gen_out.p, n);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out96, c->gen_out.p, (size_t)n * 96, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return BGV_OK;
+}
+
+// ---------------------------------------------------------------- batches
+
+static void random_scalars(uint64_t* s, uint32_t n) {
+  size_t got = 0;
+  uint8_t* p = (uint8_t*)s;
+  while (got < (size_t)n * 8) {
+    ssize_t r = getrandom(p + got, (size_t)n * 8 - got, 0);
+    if (r > 0) got += (size_t)r;
+  }
+  for (uint32_t i = 0; i < n; i++)
+    while (s[i] == 0) (void)getrandom(&s[i], 8, 0);  // blst needs non-zero randomness
+}
+
+template <class T>
+static int stage_in(bgv_ctx* c, dbuf<T>& buf, const T* src, size_t n, const T*& dst) {
+  if (int r = buf.ensure(n ? n : 1)) return r;
+  if (n) HIPCHK(hipMemcpyAsync(buf.p, src, n * sizeof(T), hipMemcpyHostToDevice, c->st));
+  dst = buf.p;
+  return 0;
+}
+
+// Build the device view of a batch: stage host arrays, convert raw pubkeys.
+static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, std::vector<uint64_t>& scal_host, bool need_sigs) {
+  if (!b) return fail(BGV_E_INVALID_ARG, "batch is NULL");
+  if (!b->job_offsets || !b->pk_offsets || !b->pk_indices || !b->msgs || (need_sigs && (!b->sigs || !b->sig_len)))
+    return fail(BGV_E_INVALID_ARG, "missing batch array");
+  if (b->n_raw && !b->raw_pks) return fail(BGV_E_INVALID_ARG, "n_raw > 0 but raw_pks is NULL");
+  const uint32_t n = b->n_sets, J = b->n_jobs;
+  memset(&d, 0, sizeof d);
+  d.n_sets = n;
+  d.n_jobs = J;
+  d.n_raw = b->n_raw;
+  d.table_n = c->table_n;
+  d.table = c->table;
+  if (!b->on_device) {
+    // host-side contract checks (the reference rejects these synchronously)
+    if (b->job_offsets[0] != 0 || b->job_offsets[J] != n) return fail(BGV_E_INVALID_ARG, "job_offsets must span [0, n_sets]");
+    for (uint32_t j = 0; j < J; j++)
+      if (b->job_offsets[j + 1] < b->job_offsets[j]) return fail(BGV_E_INVALID_ARG, "job_offsets not monotone");
+    if (b->pk_offsets[0] != 0) return fail(BGV_E_INVALID_ARG, "pk_offsets[0] != 0");
+    for (uint32_t i = 0; i < n; i++) {
+      if (b->pk_offsets[i + 1] < b->pk_offsets[i]) return fail(BGV_E_INVALID_ARG, "pk_offsets not monotone");
+      if (b->pk_offsets[i + 1] == b->pk_offsets[i]) return fail(BGV_E_EMPTY_SET, "EMPTY_AGGREGATE_ARRAY (set %u)", i);
+    }
+    const uint32_t total = b->pk_offsets[n];
+    for (uint32_t k = 0; k < total; k++) {
+      const uint32_t idx = b->pk_indices[k];
+      if (idx & 0x80000000u) {
+        if ((idx & 0x7fffffffu) >= b->n_raw) return fail(BGV_E_TABLE_RANGE, "raw pubkey index %u >= n_raw %u", idx & 0x7fffffffu, b->n_raw);
+      } else if (idx >= c->table_n) {
+        return fail(BGV_E_TABLE_RANGE, "pubkey index %u >= table size %u", idx, c->table_n);
+      }
+    }
+    if (int r = stage_in(c, c->job_off, b->job_offsets, (size_t)J + 1, d.job_off)) return r;
+    if (int r = stage_in(c, c->pk_off, b->pk_offsets, (size_t)n + 1, d.pk_off)) return r;
+    if (int r = stage_in(c, c->pk_idx, b->pk_indices, (size_t)total, d.pk_idx)) return r;
+    if (int r = stage_in(c, c->msgs, b->msgs, (size_t)n * 32, d.msgs)) return r;
+    if (need_sigs) {
+      if (int r = stage_in(c, c->sigs, b->sigs, (size_t)n * 192, d.sigs)) return r;
+      if (int r = stage_in(c, c->sig_len, b->sig_len, (size_t)n, d.sig_len)) return r;
+    }
+    const uint8_t* raw_dev = nullptr;
+    if (int r = stage_in(c, c->raw_in, b->raw_pks, (size_t)b->n_raw * 96, raw_dev)) return r;
+    if (int r = c->raw_conv.ensure(b->n_raw ? b->n_raw : 1)) return r;
+    launch_raw_pks(c->st, raw_dev, c->raw_conv.p, b->n_raw);
+    d.raw_pks = c->raw_conv.p;
+  } else {
+    d.job_off = b->job_offsets;
+    d.pk_off = b->pk_offsets;
+    d.pk_idx = b->pk_indices;
+    d.msgs = b->msgs;
+    d.sigs = b->sigs;
+    d.sig_len = b->sig_len;
+    if (int r = c->raw_conv.ensure(b->n_raw ? b->n_raw : 1)) return r;
+    launch_raw_pks(c->st, b->raw_pks, c->raw_conv.p, b->n_raw);
+    d.raw_pks = c->raw_conv.p;
+  }
+  if (b->scalars && !b->on_device) {
+    if (int r = stage_in(c, c->scalars, b->scalars, (size_t)n, d.scalars)) return r;
+  } else if (b->scalars) {
+    d.scalars = b->scalars;
+  } else {
+    scal_host.resize(n ? n : 1);
+    random_scalars(scal_host.data(), n);
+    if (int r = stage_in(c, c->scalars, (const uint64_t*)scal_host.data(), (size_t)n, d.scalars)) return r;
+  }
+  return 0;
+}
+
+static int work_alloc(bgv_ctx* c, uint32_t n, uint32_t J, dev_work& w) {
+  const size_t ns = n ? n : 1, nj = J ? J : 1;
+  int r = 0;
+  if ((r = c->sig_aff.ensure(ns)) || (r = c->h_aff.ensure(ns)) || (r = c->sig_inf.ensure(ns)) ||
+      (r = c->sig_code.ensure(ns)) || (r = c->pk_code.ensure(ns)) || (r = c->rpk_aff.ensure(ns)) ||
+      (r = c->rsig.ensure(ns)) || (r = c->f_set.ensure(ns)) || (r = c->set_code.ensure(ns)) ||
+      (r = c->f_job.ensure(nj)) || (r = c->job_code.ensure(nj)) || (r = c->job_result.ensure(nj)) ||
+      (r = c->f_part.ensure(65)) || (r = c->flags.ensure(4)))
+    return r;
+  w.sig_aff = c->sig_aff.p; w.h_aff = c->h_aff.p; w.sig_inf = c->sig_inf.p; w.sig_code = c->sig_code.p;
+  w.pk_code = c->pk_code.p; w.rpk_aff = c->rpk_aff.p; w.rsig = c->rsig.p; w.f_set = c->f_set.p;
+  w.set_code = c->set_code.p; w.f_job = c->f_job.p; w.job_code = c->job_code.p; w.job_result = c->job_result.p;
+  w.f_part = c->f_part.p; w.flags = c->flags.p;
+  return 0;
+}
+
+// run stages [from, to) with an event before each
+static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int from, int to) {
+  for (int s = from; s < to; s++) {
+    HIPCHK(hipEventRecord(c->ev[s], c->st));
+    launch_stage(c->st, s, d, w);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipEventRecord(c->ev[to], c->st));
+  return 0;
+}
+
+int bgv_verify(bgv_ctx* c, const bgv_batch* b, int32_t* job_result, int32_t* set_code, bgv_stats* stats) {
+  if (!c || !b || (!job_result && b->n_jobs)) return fail(BGV_E_INVALID_ARG, "null argument");
+  HIPCHK(hipSetDevice(c->device));
+  dev_batch d;
+  std::vector<uint64_t> scal;
+  if (int r = prepare(c, b, d, scal, true)) return r;
+  dev_work w;
+  if (int r = work_alloc(c, d.n_sets, d.n_jobs, w)) return r;
+  if (int r = run_stages(c, d, w, 0, ST_COUNT)) return r;
+  if (d.n_jobs) HIPCHK(hipMemcpyAsync(job_result, w.job_result, (size_t)d.n_jobs * 4, hipMemcpyDeviceToHost, c->st));
+  if (set_code && d.n_sets) HIPCHK(hipMemcpyAsync(set_code, w.set_code, (size_t)d.n_sets * 4, hipMemcpyDeviceToHost, c->st));
+  uint32_t flag = 0;
+  HIPCHK(hipMemcpyAsync(&flag, w.flags, 4, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  if (stats) {
+    memset(stats, 0, sizeof *stats);
+    for (int s = 0; s < ST_COUNT && s < BGV_N_STAGES; s++) HIPCHK(hipEventElapsedTime(&stats->stage_ms[s], c->ev[s], c->ev[s + 1]));
+    HIPCHK(hipEventElapsedTime(&stats->total_ms, c->ev[0], c->ev[ST_COUNT]));
+    stats->n_sets = d.n_sets;
+    stats->n_jobs = d.n_jobs;
+    uint32_t valid_jobs = 0, valid_sets = 0;
+    if (!b->on_device) {
+      for (uint32_t j = 0; j < d.n_jobs; j++)
+        if (job_result[j] >= 0) { valid_jobs++; valid_sets += b->job_offsets[j + 1] - b->job_offsets[j]; }
+      stats->pubkeys_aggregated = b->pk_offsets[d.n_sets];
+    }
+    stats->batch_retries = (valid_jobs && !flag) ? 1u : 0u;
+    stats->batch_sigs_success = flag ? valid_sets : 0u;
+  }
+  return BGV_OK;
+}
+
+// ---- multi-GPU partials ---------------------------------------------------
+static void fp12_to_bytes(uint8_t* out, const fp12_t& f) {
+  const fp2_t* cs[6] = {&f.c0.c0, &f.c1.c0, &f.c0.c1, &f.c1.c1, &f.c0.c2, &f.c1.c2};
+  for (int k = 0; k < 6; k++) {
+    fp_t t;
+    fp_from_mont(t, cs[k]->c0);
+    fp_to_be48(out + 96 * k, t);
+    fp_from_mont(t, cs[k]->c1);
+    fp_to_be48(out + 96 * k + 48, t);
+  }
+}
+
+static void fp12_from_bytes(fp12_t& f, const uint8_t* in) {
+  fp2_t* cs[6] = {&f.c0.c0, &f.c1.c0, &f.c0.c1, &f.c1.c1, &f.c0.c2, &f.c1.c2};
+  for (int k = 0; k < 6; k++) {
+    fp_t t;
+    fp_from_be48(t, in + 96 * k);
+    fp_to_mont(cs[k]->c0, t);
+    fp_from_be48(t, in + 96 * k + 48);
+    fp_to_mont(cs[k]->c1, t);
+  }
+}
+
+int bgv_partial(bgv_ctx* c, const bgv_batch* b, uint8_t* miller576, int32_t* set_code, int32_t* ok_out) {
+  if (!c || !b || !miller576) return fail(BGV_E_INVALID_ARG, "null argument");
+  HIPCHK(hipSetDevice(c->device));
+  dev_batch d;
+  std::vector<uint64_t> scal;
+  if (int r = prepare(c, b, d, scal, true)) return r;
+  dev_work w;
+  if (int r = work_alloc(c, d.n_sets, d.n_jobs, w)) return r;
+  if (int r = run_stages(c, d, w, ST_SIG, ST_BATCH_FINAL)) return r;
+  launch_stage(c->st, ST_SET_CODES, d, w);
+  HIPCHK(hipGetLastError());
+  fp12_t f;
+  HIPCHK(hipMemcpyAsync(&f, w.f_part + 64, sizeof f, hipMemcpyDeviceToHost, c->st));
+  std::vector<int32_t> jc(d.n_jobs ? d.n_jobs : 1);
+  if (d.n_jobs) HIPCHK(hipMemcpyAsync(jc.data(), w.job_code, (size_t)d.n_jobs * 4, hipMemcpyDeviceToHost, c->st));
+  if (set_code && d.n_sets) HIPCHK(hipMemcpyAsync(set_code, w.set_code, (size_t)d.n_sets * 4, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  fp12_to_bytes(miller576, f);
+  int32_t ok = 1;
+  for (uint32_t j = 0; j < d.n_jobs; j++)
+    if (jc[j] != 0) ok = 0;
+  if (ok_out) *ok_out = ok;
+  return BGV_OK;
+}
+
+int bgv_combine_final(bgv_ctx* c, const uint8_t* parts, uint32_t n, int32_t* is_one) {
+  if (!c || (!parts && n) || !is_one) return fail(BGV_E_INVALID_ARG, "null argument");
+  HIPCHK(hipSetDevice(c->device));
+  std::vector<fp12_t> h(n ? n : 1);
+  for (uint32_t k = 0; k < n; k++) fp12_from_bytes(h[k], parts + 576u * k);
+  if (int r = c->f_part.ensure(n + 65 > 65 ? n + 65 : 65)) return r;
+  if (int r = c->flags.ensure(4)) return r;
+  if (n) HIPCHK(hipMemcpyAsync(c->f_part.p, h.data(), (size_t)n * sizeof(fp12_t), hipMemcpyHostToDevice, c->st));
+  launch_combine_final(c->st, c->f_part.p, n, c->flags.p);
+  HIPCHK(hipGetLastError());
+  uint32_t flag = 0;
+  HIPCHK(hipMemcpyAsync(&flag, c->flags.p, 4, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  *is_one = flag ? 1 : 0;
+  return BGV_OK;
+}
+
+// ---- synthetic data --------------------------------------------------------
+int bgv_gen_keys(bgv_ctx* c, uint32_t first, uint32_t n, uint64_t seed) {
+  if (!c) return fail(BGV_E_INVALID_ARG, "null ctx");
+  if (n == 0) return BGV_OK;
+  HIPCHK(hipSetDevice(c->device));
+  if (int r = table_reserve(c, first + n)) return r;
+  if (c->sk.cap < (size_t)(first + n) * 8) {
+    // keep previously generated keys when growing
+    dbuf<uint32_t> nb;
+    if (int r = nb.ensure((size_t)(first + n) * 8)) return r;
+    HIPCHK(hipMemsetAsync(nb.p, 0, nb.cap * 4, c->st));
+    if (c->sk.p) HIPCHK(hipMemcpyAsync(nb.p, c->sk.p, c->sk.cap * 4, hipMemcpyDeviceToDevice, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    c->sk.release();
+    c->sk = nb;
+  }
+  launch_gen_keys(c->st, c->table, c->sk.p, first, n, seed);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->st));
+  if (first + n > c->table_n) c->table_n = first + n;
+  return BGV_OK;
+}
+
+int bgv_gen_sign(bgv_ctx* c, const bgv_batch* b, uint8_t* sigs_out) {
+  if (!c || !b || !sigs_out) return fail(BGV_E_INVALID_ARG, "null argument");
+  if (!c->sk.p) return fail(BGV_E_INVALID_ARG, "bgv_gen_keys has not run on this context");
+  HIPCHK(hipSetDevice(c->device));
+  dev_batch d;
+  std::vector<uint64_t> scal;
+  bgv_batch bb = *b;
+  bb.scalars = nullptr;
+  if (int r = prepare(c, &bb, d, scal, false)) return r;
+  uint8_t* out = sigs_out;
+  if (!b->on_device) {
+    if (int r = c->gen_out.ensure((size_t)d.n_sets * 192 + 1)) return r;
+    HIPCHK(hipMemsetAsync(c->gen_out.p, 0, (size_t)d.n_sets * 192, c->st));
+    out = c->gen_out.p;
+  }
+  launch_gen_sign(c->st, d, c->sk.p, out);
+  HIPCHK(hipGetLastError());
+  if (!b->on_device) HIPCHK(hipMemcpyAsync(sigs_out, out, (size_t)d.n_sets * 192, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return BGV_OK;
+}
+
+// ---- microbenchmarks ---------------------------------------------------------
+int bgv_bench_fpmul(bgv_ctx* c, uint32_t lanes, uint32_t iters, float* ms) {
+  if (!c || !ms || lanes == 0 || lanes % 256) return fail(BGV_E_INVALID_ARG, "lanes must be a positive multiple of 256");
+  HIPCHK(hipSetDevice(c->device));
+  if (int r = c->mb_fp.ensure((size_t)lanes * 2)) return r;
+  std::vector<fp_t> h((size_t)lanes * 2);
+  uint64_t x = 0x9e3779b97f4a7c15ull;
+  for (auto& e : h) {
+    for (int k = 0; k < NL; k++) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; e.l[k] = (uint32_t)x; }
+    e.l[NL - 1] &= 0x0fffffffu;  // < p
+  }
+  HIPCHK(hipMemcpyAsync(c->mb_fp.p, h.data(), h.size() * sizeof(fp_t), hipMemcpyHostToDevice, c->st));
+  launch_bench_fpmul(c->st, c->mb_fp.p, lanes, 16);  // warm-up
+  HIPCHK(hipEventRecord(c->ev[0], c->st));
+  launch_bench_fpmul(c->st, c->mb_fp.p, lanes, iters);
+  HIPCHK(hipEventRecord(c->ev[1], c->st));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventSynchronize(c->ev[1]));
+  HIPCHK(hipEventElapsedTime(ms, c->ev[0], c->ev[1]));
+  return BGV_OK;
+}
+
+int bgv_bench_mad(bgv_ctx* c, uint32_t lanes, uint32_t iters, float* ms) {
+  if (!c || !ms || lanes == 0 || lanes % 256) return fail(BGV_E_INVALID_ARG, "lanes must be a positive multiple of 256");
+  HIPCHK(hipSetDevice(c->device));
+  if (int r = c->mb_u64.ensure(lanes)) return r;
+  HIPCHK(hipMemsetAsync(c->mb_u64.p, 0x5a, (size_t)lanes * 8, c->st));
+  launch_bench_mad(c->st, c->mb_u64.p, lanes, 16);
+  HIPCHK(hipEventRecord(c->ev[0], c->st));
+  launch_bench_mad(c->st, c->mb_u64.p, lanes, iters);
+  HIPCHK(hipEventRecord(c->ev[1], c->st));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventSynchronize(c->ev[1]));
+  HIPCHK(hipEventElapsedTime(ms, c->ev[0], c->ev[1]));
+  return BGV_OK;
+}
+

@@ -1,0 +1,72 @@
+// Internal interface between the kernels (bgv_kernels.hip) and the host
+// orchestration behind the C ABI (bgv_api.hip).  Not installed.
+#pragma once
+#include "pairing.h"
+
+namespace bgv {
+
+// internal per-set codes beyond blst's (see include/bgv.h bgv_set_code)
+enum : int32_t {
+  C_INDEX_RANGE = 9,
+  C_EMPTY_JOB = 10,
+};
+
+// HBM layout of one batch (device pointers).  All arrays are dense and
+// indexed by set (or job); see include/bgv.h bgv_batch for their meaning.
+struct dev_batch {
+  uint32_t n_sets, n_jobs, n_raw, table_n;
+  const uint32_t* job_off;
+  const uint32_t* pk_off;
+  const uint32_t* pk_idx;
+  const g1a* raw_pks;  // Montgomery affine (converted by k_raw_pks)
+  const g1a* table;    // index2pubkey, Montgomery affine, 96 B per validator
+  const uint8_t* msgs;
+  const uint8_t* sigs;
+  const uint32_t* sig_len;
+  const uint64_t* scalars;
+};
+
+// Per-batch intermediates resident in HBM.
+struct dev_work {
+  g2a* sig_aff;       // decoded signature (affine)
+  uint32_t* sig_inf;  // signature is the identity
+  int32_t* sig_code;  // parse / subgroup outcome
+  g2a* h_aff;         // H(m)
+  g1a* rpk_aff;       // [r_i] aggregated pubkey, affine
+  int32_t* pk_code;
+  g2j* rsig;          // [r_i] sigma_i
+  fp12_t* f_set;      // per-set Miller value
+  fp12_t* f_job;      // per-job Miller product (incl. the -G1 pair)
+  int32_t* job_code;
+  int32_t* job_result;
+  int32_t* set_code;
+  fp12_t* f_part;     // [65] batch product scratch; [64] = whole batch
+  uint32_t* flags;    // [0] = whole batch verified
+};
+
+enum Stage {
+  ST_SIG = 0,
+  ST_HASH,
+  ST_PK,
+  ST_SIG_SCALE,
+  ST_MILLER,
+  ST_JOB,
+  ST_BATCH_PROD,
+  ST_BATCH_FINAL,
+  ST_JOB_FINAL,
+  ST_SET_CODES,
+  ST_COUNT
+};
+
+void launch_raw_pks(hipStream_t st, const uint8_t* raw, g1a* out, uint32_t n);
+void launch_table_from_compressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n);
+void launch_table_from_uncompressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n);
+void launch_table_export(hipStream_t st, const g1a* tab, uint8_t* out, uint32_t n);
+void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work& w);
+void launch_combine_final(hipStream_t st, const fp12_t* parts, uint32_t n, uint32_t* flag);
+void launch_gen_keys(hipStream_t st, g1a* table, uint32_t* sk, uint32_t first, uint32_t n, uint64_t seed);
+void launch_gen_sign(hipStream_t st, const dev_batch& b, const uint32_t* sk, uint8_t* out);
+void launch_bench_fpmul(hipStream_t st, fp_t* io, uint32_t lanes, uint32_t iters);
+void launch_bench_mad(hipStream_t st, uint64_t* io, uint32_t lanes, uint32_t iters);
+
+}  // namespace bgv

@@ -1,0 +1,477 @@
+// HIP kernels of the gfx950 BLS12-381 batch verifier.
+//
+// One device batch flows through these stages on the context's stream
+// (host orchestration: bgv_api.hip).  Every stage is one lane per signature
+// set (or per job): the per-set work is a long chain of dependent 384-bit
+// Montgomery products on the integer VALU, so the lane is the natural unit
+// and sets are independent.
+//
+//   k_raw_pks     raw (non-table) pubkeys  -> Montgomery affine G1
+//   k_sig         Signature.fromBytes(sig, affine, validate=true)
+//                 (maybeBatch.ts:23,36): length check, ZCash decode,
+//                 on-curve, G2 subgroup check (psi(P) == [x]P)
+//   k_hash        hash_to_G2(signingRoot, POP DST) -> affine H(m)
+//   k_pk          PublicKey.aggregate (chain/bls/utils.ts:11) as a gather
+//                 from the HBM index2pubkey table + [r_i] PK_i (mul_n_aggregate)
+//   k_sig_scale   [r_i] sigma_i
+//   k_miller      f_i = MillerLoop([r_i] PK_i, H(m_i))
+//   k_job         per job: f_j = prod f_i * MillerLoop(-G1, sum [r_i] sigma_i),
+//                 first parse error of the job (set order)
+//   k_batch_final whole-batch product + ONE final exponentiation
+//   k_job_final   per-job final exponentiation only if the batch check failed
+//                 (the worker's per-job retry, multithread/worker.ts:74-85)
+#include "bgv_internal.h"
+
+namespace bgv {
+
+__device__ __forceinline__ uint32_t gtid() { return blockIdx.x * blockDim.x + threadIdx.x; }
+
+// ---------------------------------------------------------------- helpers
+BGV_HD bool g1a_is_zero(const g1a& p) { return fp_is_zero(p.x) && fp_is_zero(p.y); }
+
+__device__ __forceinline__ void load_pk(g1a& out, const dev_batch& b, uint32_t idx, bool& range_err) {
+  if (idx & 0x80000000u) {
+    const uint32_t r = idx & 0x7fffffffu;
+    if (r >= b.n_raw) { range_err = true; fp_set_zero(out.x); fp_set_zero(out.y); return; }
+    out = b.raw_pks[r];
+  } else {
+    if (idx >= b.table_n) { range_err = true; fp_set_zero(out.x); fp_set_zero(out.y); return; }
+    out = b.table[idx];
+  }
+}
+
+// ------------------------------------------------------------ k_raw_pks
+// uncompressed 96 B big-endian, trusted (multithread/worker.ts:108-114:
+// PublicKey.fromBytes(.., affine) without validation); infinity -> (0, 0)
+__global__ void __launch_bounds__(64) k_raw_pks(const uint8_t* raw, g1a* out, uint32_t n) {
+  const uint32_t i = gtid();
+  if (i >= n) return;
+  g1a p;
+  if (!g1_from_uncompressed_trusted(p, raw + 96u * i)) { fp_set_zero(p.x); fp_set_zero(p.y); }
+  out[i] = p;
+}
+
+// compressed 48 B table load (syncPubkeys path); bad keys -> (0, 0)
+__global__ void __launch_bounds__(64) k_table_from_compressed(const uint8_t* in48, g1a* out, uint32_t n) {
+  const uint32_t i = gtid();
+  if (i >= n) return;
+  g1a p;
+  bool inf;
+  if (g1_decompress(p, inf, in48 + 48u * i) != C_OK || inf) { fp_set_zero(p.x); fp_set_zero(p.y); }
+  out[i] = p;
+}
+
+__global__ void __launch_bounds__(64) k_table_from_uncompressed(const uint8_t* in96, g1a* out, uint32_t n) {
+  const uint32_t i = gtid();
+  if (i >= n) return;
+  g1a p;
+  if (!g1_from_uncompressed_trusted(p, in96 + 96u * i)) { fp_set_zero(p.x); fp_set_zero(p.y); }
+  out[i] = p;
+}
+
+__global__ void __launch_bounds__(64) k_table_export(const g1a* tab, uint8_t* out96, uint32_t n) {
+  const uint32_t i = gtid();
+  if (i >= n) return;
+  const g1a p = tab[i];
+  uint8_t* o = out96 + 96u * i;
+  if (g1a_is_zero(p)) {
+    for (int k = 0; k < 96; k++) o[k] = 0;
+    o[0] = 0x40;
+    return;
+  }
+  fp_t t;
+  fp_from_mont(t, p.x);
+  fp_to_be48(o, t);
+  fp_from_mont(t, p.y);
+  fp_to_be48(o + 48, t);
+}
+
+// ------------------------------------------------------------------ k_sig
+__global__ void __launch_bounds__(64) k_sig(dev_batch b, dev_work w) {
+  const uint32_t i = gtid();
+  if (i >= b.n_sets) return;
+  const uint32_t len = b.sig_len[i];
+  const uint8_t* s = b.sigs + 192u * i;
+  g2a a;
+  bool inf = false;
+  int32_t code;
+  if (len == 96u) code = g2_decompress(a, inf, s);
+  else if (len == 192u) code = g2_deserialize(a, inf, s);
+  else code = C_INVALID_SIZE;
+  if (code == C_OK && !inf) {
+    g2j j;
+    jac_from_aff(j, a);
+    if (!g2_in_subgroup(j)) code = C_POINT_NOT_IN_GROUP;
+  }
+  if (code != C_OK || inf) { a.x = fp2_zero(); a.y = fp2_zero(); }
+  w.sig_aff[i] = a;
+  w.sig_inf[i] = inf ? 1u : 0u;
+  w.sig_code[i] = code;
+}
+
+// ----------------------------------------------------------------- k_hash
+__global__ void __launch_bounds__(64) k_hash(dev_batch b, dev_work w) {
+  const uint32_t i = gtid();
+  if (i >= b.n_sets) return;
+  uint8_t m[32];
+#pragma unroll
+  for (int k = 0; k < 32; k++) m[k] = b.msgs[32u * i + k];
+  g2j h;
+  hash_to_g2(h, m);
+  g2a ha;
+  jac_to_aff(ha, h);  // H(m) is never the identity for a 32-byte root (prob. 2^-255)
+  w.h_aff[i] = ha;
+}
+
+// ------------------------------------------------------------------- k_pk
+__global__ void __launch_bounds__(64) k_pk(dev_batch b, dev_work w) {
+  const uint32_t i = gtid();
+  if (i >= b.n_sets) return;
+  const uint32_t beg = b.pk_off[i], end = b.pk_off[i + 1];
+  g1j acc;
+  jac_set_inf(acc);
+  bool range_err = false;
+  for (uint32_t k = beg; k < end; k++) {
+    g1a p;
+    load_pk(p, b, b.pk_idx[k], range_err);
+    if (g1a_is_zero(p)) continue;  // infinity entry adds nothing
+    jac_add_aff(acc, acc, p);
+  }
+  int32_t code = C_OK;
+  if (range_err) code = C_INDEX_RANGE;
+  else if (jac_is_inf(acc)) code = C_PK_IS_INFINITY;
+  g1a out;
+  if (code == C_OK) {
+    g1j rp;
+    jac_mul_u64(rp, acc, b.scalars[i]);
+    jac_to_aff(out, rp);
+  } else {
+    fp_set_zero(out.x); fp_set_zero(out.y);
+  }
+  w.rpk_aff[i] = out;
+  w.pk_code[i] = code;
+}
+
+// ------------------------------------------------------------ k_sig_scale
+__global__ void __launch_bounds__(64) k_sig_scale(dev_batch b, dev_work w) {
+  const uint32_t i = gtid();
+  if (i >= b.n_sets) return;
+  g2j r;
+  if (w.sig_code[i] != C_OK || w.sig_inf[i]) {
+    jac_set_inf(r);  // infinity signature: blst skips it (adds the identity)
+  } else {
+    g2j s;
+    jac_from_aff(s, w.sig_aff[i]);
+    jac_mul_u64(r, s, b.scalars[i]);
+  }
+  w.rsig[i] = r;
+}
+
+// --------------------------------------------------------------- k_miller
+__global__ void __launch_bounds__(64) k_miller(dev_batch b, dev_work w) {
+  const uint32_t i = gtid();
+  if (i >= b.n_sets) return;
+  fp12_t f;
+  if (w.sig_code[i] != C_OK || w.pk_code[i] != C_OK) {
+    fp12_one(f);
+  } else {
+    miller_loop(f, w.rpk_aff[i], false, w.h_aff[i], false);
+  }
+  w.f_set[i] = f;
+}
+
+// ------------------------------------------------------------------ k_job
+__global__ void __launch_bounds__(64) k_job(dev_batch b, dev_work w) {
+  const uint32_t j = gtid();
+  if (j >= b.n_jobs) return;
+  const uint32_t beg = b.job_off[j], end = b.job_off[j + 1];
+  // reference order: every signature of the job is parsed/validated first
+  // (maybeBatch.ts:20-24 sets.map(fromBytes)), then blst reaches the pubkeys
+  int32_t code = C_OK;
+  for (uint32_t i = beg; i < end && code == C_OK; i++) code = w.sig_code[i];
+  for (uint32_t i = beg; i < end && code == C_OK; i++) code = w.pk_code[i];
+  if (end == beg) code = C_EMPTY_JOB;
+  fp12_t f;
+  fp12_one(f);
+  if (code == C_OK) {
+    g2j s;
+    jac_set_inf(s);
+    bool first = true;
+    for (uint32_t i = beg; i < end; i++) {
+      const g2j r = w.rsig[i];
+      jac_add(s, s, r);
+      if (first) { f = w.f_set[i]; first = false; }
+      else fp12_mul(f, f, w.f_set[i]);
+    }
+    g2a sa;
+    if (jac_to_aff(sa, s)) {
+      g1a ng;
+      ng.x = G1_X_MONT;
+      ng.y = G1_NEG_Y_MONT;
+      fp12_t g;
+      miller_loop(g, ng, false, sa, false);
+      fp12_mul(f, f, g);
+    }
+  }
+  w.f_job[j] = f;
+  w.job_code[j] = code;
+}
+
+// ---------------------------------------------------------- k_batch_final
+// One workgroup of 64 lanes: lane l multiplies jobs l, l+64, ...; lane 0
+// folds the 64 partials and runs the single final exponentiation.
+__global__ void __launch_bounds__(64) k_batch_prod(dev_batch b, dev_work w) {
+  const uint32_t l = threadIdx.x;
+  fp12_t f;
+  fp12_one(f);
+  bool any = false;
+  for (uint32_t j = l; j < b.n_jobs; j += 64) {
+    if (w.job_code[j] != C_OK) continue;
+    if (!any) { f = w.f_job[j]; any = true; }
+    else fp12_mul(f, f, w.f_job[j]);
+  }
+  w.f_part[l] = f;
+  __syncthreads();
+  if (l != 0) return;
+  fp12_t g = w.f_part[0];
+  for (int k = 1; k < 64; k++) fp12_mul(g, g, w.f_part[k]);
+  w.f_part[64] = g;
+}
+
+__global__ void __launch_bounds__(64) k_batch_final(dev_batch b, dev_work w) {
+  if (threadIdx.x != 0) return;
+  fp12_t r;
+  fp12_final_exp(r, w.f_part[64]);
+  w.flags[0] = fp12_is_one(r) ? 1u : 0u;
+}
+
+// ------------------------------------------------------------ k_job_final
+__global__ void __launch_bounds__(64) k_job_final(dev_batch b, dev_work w) {
+  const uint32_t j = gtid();
+  if (j >= b.n_jobs) return;
+  const int32_t code = w.job_code[j];
+  int32_t res;
+  if (code != C_OK) {
+    res = -code;
+  } else if (w.flags[0]) {
+    res = 1;  // whole batch verified: every job is valid
+  } else {
+    fp12_t r;
+    fp12_final_exp(r, w.f_job[j]);
+    res = fp12_is_one(r) ? 1 : 0;
+  }
+  w.job_result[j] = res;
+}
+
+// set codes for the host: signature code first, then the pubkey code
+__global__ void __launch_bounds__(64) k_set_codes(dev_batch b, dev_work w) {
+  const uint32_t i = gtid();
+  if (i >= b.n_sets) return;
+  const int32_t c = w.sig_code[i];
+  w.set_code[i] = c != C_OK ? c : w.pk_code[i];
+}
+
+// ------------------------------------------------- multi-GPU combination
+__global__ void __launch_bounds__(64) k_combine_final(const fp12_t* parts, uint32_t n, uint32_t* flag) {
+  if (threadIdx.x != 0) return;
+  fp12_t g;
+  fp12_one(g);
+  for (uint32_t k = 0; k < n; k++) fp12_mul(g, g, parts[k]);
+  fp12_t r;
+  fp12_final_exp(r, g);
+  flag[0] = fp12_is_one(r) ? 1u : 0u;
+}
+
+// ======================================================= synthetic data
+// scalar field order r (little-endian u32)
+BGV_CONST uint32_t FR_R[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
+                              0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
+
+BGV_HD bool u256_ge_r(const uint32_t a[8]) {
+  for (int i = 7; i >= 0; i--) {
+    if (a[i] > FR_R[i]) return true;
+    if (a[i] < FR_R[i]) return false;
+  }
+  return true;
+}
+
+BGV_HD void u256_sub_r(uint32_t a[8]) {
+  uint32_t borrow = 0;
+  for (int i = 0; i < 8; i++) {
+    uint64_t d = (uint64_t)a[i] - FR_R[i] - borrow;
+    a[i] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+}
+
+// a = (a + b) mod r, both < r
+BGV_HD void fr_add(uint32_t a[8], const uint32_t b[8]) {
+  uint32_t c = 0;
+  for (int i = 0; i < 8; i++) {
+    uint64_t s = (uint64_t)a[i] + b[i] + c;
+    a[i] = (uint32_t)s;
+    c = (uint32_t)(s >> 32);
+  }
+  if (u256_ge_r(a)) u256_sub_r(a);
+}
+
+// [k]P, k = 256-bit little-endian u32 words, left-to-right double-and-add
+template <class F>
+BGV_NI void jac_mul_u256(jac_t<F>& r, const jac_t<F>& p, const uint32_t k[8]) {
+  jac_t<F> acc;
+  jac_set_inf(acc);
+  for (int w = 7; w >= 0; w--) {
+    for (int bit = 31; bit >= 0; bit--) {
+      jac_dbl(acc, acc);
+      if ((k[w] >> bit) & 1u) jac_add(acc, acc, p);
+    }
+  }
+  r = acc;
+}
+
+// sk_i = SHA256("bgv-sk" || LE64(seed) || LE32(i)) (big-endian integer) mod r
+__device__ void gen_sk(uint32_t sk[8], uint64_t seed, uint32_t i) {
+  uint32_t blk[16];
+  blk_clear(blk);
+  const char tag[6] = {'b', 'g', 'v', '-', 's', 'k'};
+  int pos = 0;
+  for (int k = 0; k < 6; k++) blk_put(blk, pos++, (uint8_t)tag[k]);
+  for (int k = 0; k < 8; k++) blk_put(blk, pos++, (uint32_t)(seed >> (8 * k)));
+  for (int k = 0; k < 4; k++) blk_put(blk, pos++, (i >> (8 * k)));
+  blk_put(blk, pos, 0x80);
+  blk[15] = (uint32_t)pos * 8u;  // 18 bytes
+  uint32_t st[8];
+  for (int k = 0; k < 8; k++) st[k] = SHA256_IV[k];
+  sha256_compress(st, blk);
+  // digest words are big-endian: st[0] is the most significant
+  for (int k = 0; k < 8; k++) sk[k] = st[7 - k];
+  while (u256_ge_r(sk)) u256_sub_r(sk);
+}
+
+__global__ void __launch_bounds__(64) k_gen_keys(g1a* table, uint32_t* sk_store, uint32_t first, uint32_t n,
+                                                 uint64_t seed) {
+  const uint32_t t = gtid();
+  if (t >= n) return;
+  const uint32_t i = first + t;
+  uint32_t sk[8];
+  gen_sk(sk, seed, i);
+  for (int k = 0; k < 8; k++) sk_store[8u * i + k] = sk[k];
+  g1j g, p;
+  g.x = G1_X_MONT; g.y = G1_Y_MONT; fe_one(g.z);
+  jac_mul_u256(p, g, sk);
+  g1a a;
+  jac_to_aff(a, p);
+  table[i] = a;
+}
+
+BGV_NI void g2_compress(uint8_t* out, const g2j& p) {
+  g2a a;
+  if (!jac_to_aff(a, p)) {
+    for (int k = 0; k < 96; k++) out[k] = 0;
+    out[0] = 0xc0;
+    return;
+  }
+  uint8_t buf[96];
+  fp_t t;
+  fp_from_mont(t, a.x.c1);
+  fp_to_be48(buf, t);
+  fp_from_mont(t, a.x.c0);
+  fp_to_be48(buf + 48, t);
+  buf[0] |= 0x80u | (fp2_lex_largest(a.y) ? 0x20u : 0u);
+  for (int k = 0; k < 96; k++) out[k] = buf[k];
+}
+
+__global__ void __launch_bounds__(64) k_gen_sign(dev_batch b, const uint32_t* sk_store, uint8_t* sigs_out) {
+  const uint32_t i = gtid();
+  if (i >= b.n_sets) return;
+  uint32_t s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint32_t k = b.pk_off[i]; k < b.pk_off[i + 1]; k++) {
+    const uint32_t idx = b.pk_idx[k];
+    if (idx >= b.table_n) continue;
+    uint32_t sk[8];
+    for (int q = 0; q < 8; q++) sk[q] = sk_store[8u * idx + q];
+    fr_add(s, sk);
+  }
+  uint8_t m[32];
+  for (int k = 0; k < 32; k++) m[k] = b.msgs[32u * i + k];
+  g2j h, sig;
+  hash_to_g2(h, m);
+  jac_mul_u256(sig, h, s);
+  g2_compress(sigs_out + 192u * i, sig);
+}
+
+// ========================================================= microbenchmarks
+__global__ void __launch_bounds__(256) k_bench_fpmul(fp_t* io, uint32_t iters) {
+  const uint32_t i = gtid();
+  fp_t x = io[2 * i], y = io[2 * i + 1];
+  for (uint32_t k = 0; k < iters; k++) fp_mul(x, x, y);
+  io[2 * i] = x;
+}
+
+__global__ void __launch_bounds__(256) k_bench_mad(uint64_t* io, uint32_t iters) {
+  const uint32_t i = gtid();
+  uint64_t a0 = io[i], a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  const uint32_t m = (uint32_t)a0 | 1u;
+  for (uint32_t k = 0; k < iters; k++) {
+    a0 = (uint64_t)(uint32_t)a0 * m + (a0 >> 32);
+    a1 = (uint64_t)(uint32_t)a1 * m + (a1 >> 32);
+    a2 = (uint64_t)(uint32_t)a2 * m + (a2 >> 32);
+    a3 = (uint64_t)(uint32_t)a3 * m + (a3 >> 32);
+    a4 = (uint64_t)(uint32_t)a4 * m + (a4 >> 32);
+    a5 = (uint64_t)(uint32_t)a5 * m + (a5 >> 32);
+    a6 = (uint64_t)(uint32_t)a6 * m + (a6 >> 32);
+    a7 = (uint64_t)(uint32_t)a7 * m + (a7 >> 32);
+  }
+  io[i] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+
+// ============================================================= launchers
+static inline dim3 grid64(uint32_t n) { return dim3((n + 63u) / 64u); }
+
+#define BGV_LAUNCH(k, n, ...)                                                 \
+  do {                                                                        \
+    if ((n) > 0) hipLaunchKernelGGL(k, grid64(n), dim3(64), 0, st, __VA_ARGS__); \
+  } while (0)
+
+void launch_raw_pks(hipStream_t st, const uint8_t* raw, g1a* out, uint32_t n) { BGV_LAUNCH(k_raw_pks, n, raw, out, n); }
+void launch_table_from_compressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n) {
+  BGV_LAUNCH(k_table_from_compressed, n, in, out, n);
+}
+void launch_table_from_uncompressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n) {
+  BGV_LAUNCH(k_table_from_uncompressed, n, in, out, n);
+}
+void launch_table_export(hipStream_t st, const g1a* tab, uint8_t* out, uint32_t n) {
+  BGV_LAUNCH(k_table_export, n, tab, out, n);
+}
+void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work& w) {
+  switch (stage) {
+    case ST_SIG: BGV_LAUNCH(k_sig, b.n_sets, b, w); break;
+    case ST_HASH: BGV_LAUNCH(k_hash, b.n_sets, b, w); break;
+    case ST_PK: BGV_LAUNCH(k_pk, b.n_sets, b, w); break;
+    case ST_SIG_SCALE: BGV_LAUNCH(k_sig_scale, b.n_sets, b, w); break;
+    case ST_MILLER: BGV_LAUNCH(k_miller, b.n_sets, b, w); break;
+    case ST_JOB: BGV_LAUNCH(k_job, b.n_jobs, b, w); break;
+    case ST_BATCH_PROD: hipLaunchKernelGGL(k_batch_prod, dim3(1), dim3(64), 0, st, b, w); break;
+    case ST_BATCH_FINAL: hipLaunchKernelGGL(k_batch_final, dim3(1), dim3(64), 0, st, b, w); break;
+    case ST_JOB_FINAL: BGV_LAUNCH(k_job_final, b.n_jobs, b, w); break;
+    case ST_SET_CODES: BGV_LAUNCH(k_set_codes, b.n_sets, b, w); break;
+    default: break;
+  }
+}
+void launch_combine_final(hipStream_t st, const fp12_t* parts, uint32_t n, uint32_t* flag) {
+  hipLaunchKernelGGL(k_combine_final, dim3(1), dim3(64), 0, st, parts, n, flag);
+}
+void launch_gen_keys(hipStream_t st, g1a* table, uint32_t* sk, uint32_t first, uint32_t n, uint64_t seed) {
+  BGV_LAUNCH(k_gen_keys, n, table, sk, first, n, seed);
+}
+void launch_gen_sign(hipStream_t st, const dev_batch& b, const uint32_t* sk, uint8_t* out) {
+  BGV_LAUNCH(k_gen_sign, b.n_sets, b, sk, out);
+}
+void launch_bench_fpmul(hipStream_t st, fp_t* io, uint32_t lanes, uint32_t iters) {
+  hipLaunchKernelGGL(k_bench_fpmul, dim3(lanes / 256), dim3(256), 0, st, io, iters);
+}
+void launch_bench_mad(hipStream_t st, uint64_t* io, uint32_t lanes, uint32_t iters) {
+  hipLaunchKernelGGL(k_bench_mad, dim3(lanes / 256), dim3(256), 0, st, io, iters);
+}
+
+}  // namespace bgv

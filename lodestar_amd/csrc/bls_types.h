@@ -9,10 +9,12 @@
 #define BGV_HD __host__ __device__ __forceinline__
 #define BGV_HDN __host__ __device__ __noinline__
 #define BGV_CONST __constant__ const
+#define BGV_NI static __host__ __device__ __noinline__
 #else
 #define BGV_HD static inline
 #define BGV_HDN static
 #define BGV_CONST static const
+#define BGV_NI static inline
 #endif
 
 namespace bgv {

@@ -57,7 +57,7 @@ template <class F> BGV_HD void jac_neg(jac_t<F>& r, const jac_t<F>& p) {
 }
 
 // dbl-2009-l (a = 0): 2M + 5S
-template <class F> BGV_HD void jac_dbl(jac_t<F>& r, const jac_t<F>& p) {
+template <class F> BGV_NI void jac_dbl(jac_t<F>& r, const jac_t<F>& p) {
   F A, B, C, D, E, Fq, t;
   fe_sqr(A, p.x);
   fe_sqr(B, p.y);
@@ -83,7 +83,7 @@ template <class F> BGV_HD void jac_dbl(jac_t<F>& r, const jac_t<F>& p) {
 }
 
 // add-2007-bl with the exceptional cases (infinity, P == Q, P == -Q)
-template <class F> BGV_HD void jac_add(jac_t<F>& r, const jac_t<F>& p, const jac_t<F>& q) {
+template <class F> BGV_NI void jac_add(jac_t<F>& r, const jac_t<F>& p, const jac_t<F>& q) {
   if (jac_is_inf(p)) { r = q; return; }
   if (jac_is_inf(q)) { r = p; return; }
   F z1z1, z2z2, u1, u2, s1, s2, h, i, j, rr, v, t;
@@ -126,7 +126,7 @@ template <class F> BGV_HD void jac_add(jac_t<F>& r, const jac_t<F>& p, const jac
 }
 
 // madd-2007-bl: Jacobian + affine (q not infinity), with exceptional cases
-template <class F> BGV_HD void jac_add_aff(jac_t<F>& r, const jac_t<F>& p, const aff_t<F>& q) {
+template <class F> BGV_NI void jac_add_aff(jac_t<F>& r, const jac_t<F>& p, const aff_t<F>& q) {
   if (jac_is_inf(p)) { jac_from_aff(r, q); return; }
   F z1z1, u2, s2, h, hh, i, j, rr, v, t;
   fe_sqr(z1z1, p.z);
@@ -164,7 +164,7 @@ template <class F> BGV_HD void jac_add_aff(jac_t<F>& r, const jac_t<F>& p, const
 }
 
 // [k]P for a public/random 64-bit scalar k (left-to-right double-and-add)
-template <class F> BGV_HD void jac_mul_u64(jac_t<F>& r, const jac_t<F>& p, uint64_t k) {
+template <class F> BGV_NI void jac_mul_u64(jac_t<F>& r, const jac_t<F>& p, uint64_t k) {
   jac_t<F> acc;
   jac_set_inf(acc);
   if (k == 0) { r = acc; return; }
@@ -179,7 +179,7 @@ template <class F> BGV_HD void jac_mul_u64(jac_t<F>& r, const jac_t<F>& p, uint6
 }
 
 // [|x|]P for the BLS parameter (Hamming weight 6)
-template <class F> BGV_HD void jac_mul_abs_x(jac_t<F>& r, const jac_t<F>& p) {
+template <class F> BGV_NI void jac_mul_abs_x(jac_t<F>& r, const jac_t<F>& p) {
   jac_t<F> acc = p;
   for (int b = 62; b >= 0; b--) {
     jac_dbl(acc, acc);
@@ -188,7 +188,7 @@ template <class F> BGV_HD void jac_mul_abs_x(jac_t<F>& r, const jac_t<F>& p) {
   r = acc;
 }
 
-template <class F> BGV_HD bool jac_to_aff(aff_t<F>& r, const jac_t<F>& p) {
+template <class F> BGV_NI bool jac_to_aff(aff_t<F>& r, const jac_t<F>& p) {
   if (jac_is_inf(p)) { fe_zero(r.x); fe_zero(r.y); return false; }
   F zi, zi2, zi3;
   fe_inv(zi, p.z);
@@ -200,7 +200,7 @@ template <class F> BGV_HD bool jac_to_aff(aff_t<F>& r, const jac_t<F>& p) {
 }
 
 // equality of two Jacobian points (cross-multiplied)
-template <class F> BGV_HD bool jac_eq(const jac_t<F>& p, const jac_t<F>& q) {
+template <class F> BGV_NI bool jac_eq(const jac_t<F>& p, const jac_t<F>& q) {
   const bool pi = jac_is_inf(p), qi = jac_is_inf(q);
   if (pi || qi) return pi && qi;
   F z1z1, z2z2, a, b;
@@ -241,7 +241,7 @@ BGV_HD void g2_psi2(g2j& r, const g2j& p) {
 }
 
 // Scott's test: P in G2  <=>  psi(P) == [x]P  (x = -|x|)
-BGV_HD bool g2_in_subgroup(const g2j& p) {
+BGV_NI bool g2_in_subgroup(const g2j& p) {
   if (jac_is_inf(p)) return true;
   g2j xp, ps;
   jac_mul_abs_x(xp, p);
@@ -260,7 +260,7 @@ BGV_HD bool g2_aff_on_curve(const g2a& a) {
 }
 
 // h_eff [P] = [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P)  (Budroni-Pintore)
-BGV_HD void g2_clear_cofactor(g2j& r, const g2j& p) {
+BGV_NI void g2_clear_cofactor(g2j& r, const g2j& p) {
   g2j t1, t2, t3, np;
   jac_mul_abs_x(t1, p);
   jac_neg(t1, t1);            // [x]P
@@ -281,62 +281,62 @@ BGV_HD void g2_clear_cofactor(g2j& r, const g2j& p) {
 // ---- serialization ---------------------------------------------------------
 // blst error codes (bindings/blst.h BLST_ERROR) + @chainsafe/blst size error
 enum : int32_t {
-  BGV_OK = 0,
-  BGV_BAD_ENCODING = 1,
-  BGV_POINT_NOT_ON_CURVE = 2,
-  BGV_POINT_NOT_IN_GROUP = 3,
-  BGV_AGGR_TYPE_MISMATCH = 4,
-  BGV_VERIFY_FAIL = 5,
-  BGV_PK_IS_INFINITY = 6,
-  BGV_BAD_SCALAR = 7,
-  BGV_INVALID_SIZE = 8,
+  C_OK = 0,
+  C_BAD_ENCODING = 1,
+  C_POINT_NOT_ON_CURVE = 2,
+  C_POINT_NOT_IN_GROUP = 3,
+  C_AGGR_TYPE_MISMATCH = 4,
+  C_VERIFY_FAIL = 5,
+  C_PK_IS_INFINITY = 6,
+  C_BAD_SCALAR = 7,
+  C_INVALID_SIZE = 8,
 };
 
 // ZCash 96-byte compressed G2 -> affine (Montgomery) ; returns BGV_* code.
 // *inf set for the canonical infinity encoding.
-BGV_HD int32_t g2_decompress(g2a& out, bool& inf, const uint8_t* b) {
+BGV_NI int32_t g2_decompress(g2a& out, bool& inf, const uint8_t* b) {
   inf = false;
   const uint8_t b0 = b[0];
-  if (!(b0 & 0x80)) return BGV_BAD_ENCODING;
+  if (!(b0 & 0x80)) return C_BAD_ENCODING;
   if (b0 & 0x40) {
     uint32_t acc = b0 & 0x3f;
     for (int i = 1; i < 96; i++) acc |= b[i];
-    if (acc) return BGV_BAD_ENCODING;
+    if (acc) return C_BAD_ENCODING;
     inf = true;
     out.x = fp2_zero(); out.y = fp2_zero();
-    return BGV_OK;
+    return C_OK;
   }
   fp_t x1, x0;
   fp_from_be48(x1, b);
   x1.l[NL - 1] &= 0x1fffffffu;  // clear the 3 flag bits
   fp_from_be48(x0, b + 48);
-  if (!fp_plain_lt_p(x1) || !fp_plain_lt_p(x0)) return BGV_BAD_ENCODING;
+  if (!fp_plain_lt_p(x1) || !fp_plain_lt_p(x0)) return C_BAD_ENCODING;
   fp2_t x, y2, y;
   fp_to_mont(x.c0, x0);
   fp_to_mont(x.c1, x1);
   fp2_sqr(y2, x);
   fp2_mul(y2, y2, x);
   fp2_add(y2, y2, B2_MONT);
-  if (!fp2_sqrt(y, y2)) return BGV_POINT_NOT_ON_CURVE;
+  if (!fp2_sqrt(y, y2)) return C_POINT_NOT_ON_CURVE;
   const bool want_large = (b0 & 0x20) != 0;
   if (fp2_lex_largest(y) != want_large) fp2_neg(y, y);
   out.x = x;
   out.y = y;
-  return BGV_OK;
+  return C_OK;
 }
 
 // 192-byte uncompressed G2 (blst POINTonE2_Deserialize_Z)
-BGV_HD int32_t g2_deserialize(g2a& out, bool& inf, const uint8_t* b) {
+BGV_NI int32_t g2_deserialize(g2a& out, bool& inf, const uint8_t* b) {
   inf = false;
   const uint8_t b0 = b[0];
-  if (b0 & 0x80) return BGV_BAD_ENCODING;
+  if (b0 & 0x80) return C_BAD_ENCODING;
   if (b0 & 0x40) {
     uint32_t acc = b0 & 0x3f;
     for (int i = 1; i < 192; i++) acc |= b[i];
-    if (acc) return BGV_BAD_ENCODING;
+    if (acc) return C_BAD_ENCODING;
     inf = true;
     out.x = fp2_zero(); out.y = fp2_zero();
-    return BGV_OK;
+    return C_OK;
   }
   fp_t x1, x0, y1, y0;
   fp_from_be48(x1, b);
@@ -344,13 +344,13 @@ BGV_HD int32_t g2_deserialize(g2a& out, bool& inf, const uint8_t* b) {
   fp_from_be48(x0, b + 48);
   fp_from_be48(y1, b + 96);
   fp_from_be48(y0, b + 144);
-  if (!fp_plain_lt_p(x1) || !fp_plain_lt_p(x0) || !fp_plain_lt_p(y1) || !fp_plain_lt_p(y0)) return BGV_BAD_ENCODING;
+  if (!fp_plain_lt_p(x1) || !fp_plain_lt_p(x0) || !fp_plain_lt_p(y1) || !fp_plain_lt_p(y0)) return C_BAD_ENCODING;
   fp_to_mont(out.x.c0, x0);
   fp_to_mont(out.x.c1, x1);
   fp_to_mont(out.y.c0, y0);
   fp_to_mont(out.y.c1, y1);
-  if (!g2_aff_on_curve(out)) return BGV_POINT_NOT_ON_CURVE;
-  return BGV_OK;
+  if (!g2_aff_on_curve(out)) return C_POINT_NOT_ON_CURVE;
+  return C_OK;
 }
 
 // 96-byte uncompressed G1 (x || y big-endian, the pool's PointFormat.uncompressed,
@@ -368,32 +368,32 @@ BGV_HD bool g1_from_uncompressed_trusted(g1a& out, const uint8_t* b) {
 }
 
 // 48-byte compressed G1 (trusted table entry: decompress, no subgroup check)
-BGV_HD int32_t g1_decompress(g1a& out, bool& inf, const uint8_t* b) {
+BGV_NI int32_t g1_decompress(g1a& out, bool& inf, const uint8_t* b) {
   inf = false;
   const uint8_t b0 = b[0];
-  if (!(b0 & 0x80)) return BGV_BAD_ENCODING;
+  if (!(b0 & 0x80)) return C_BAD_ENCODING;
   if (b0 & 0x40) {
     uint32_t acc = b0 & 0x3f;
     for (int i = 1; i < 48; i++) acc |= b[i];
-    if (acc) return BGV_BAD_ENCODING;
+    if (acc) return C_BAD_ENCODING;
     inf = true;
     fp_set_zero(out.x); fp_set_zero(out.y);
-    return BGV_OK;
+    return C_OK;
   }
   fp_t x;
   fp_from_be48(x, b);
   x.l[NL - 1] &= 0x1fffffffu;
-  if (!fp_plain_lt_p(x)) return BGV_BAD_ENCODING;
+  if (!fp_plain_lt_p(x)) return C_BAD_ENCODING;
   fp_t xm, y2, y;
   fp_to_mont(xm, x);
   fp_sqr(y2, xm);
   fp_mul(y2, y2, xm);
   fp_add(y2, y2, B1_MONT);
-  if (!fp_sqrt(y, y2)) return BGV_POINT_NOT_ON_CURVE;
+  if (!fp_sqrt(y, y2)) return C_POINT_NOT_ON_CURVE;
   if (fp_lex_largest(y) != ((b0 & 0x20) != 0)) fp_neg(y, y);
   out.x = xm;
   out.y = y;
-  return BGV_OK;
+  return C_OK;
 }
 
 }  // namespace bgv

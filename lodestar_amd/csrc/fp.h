@@ -145,7 +145,7 @@ BGV_HD void fp_half(fp_t& r, const fp_t& a) { fp_mul(r, a, FP_HALF); }
 // r = a^e for a fixed public exponent e (12 x u32, plain integer).
 // Left-to-right binary over the exponent's bits; the bit test is uniform
 // across the wavefront (same constant for every lane), so no divergence.
-BGV_HD void fp_pow(fp_t& r, const fp_t& a, const fp_t& e) {
+BGV_NI void fp_pow(fp_t& r, const fp_t& a, const fp_t& e) {
   fp_t acc = FP_ONE;
   bool started = false;
   for (int i = NL - 1; i >= 0; i--) {

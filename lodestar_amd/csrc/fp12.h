@@ -30,7 +30,7 @@ BGV_HD void fp6_mul_v(fp6_t& r, const fp6_t& a) {
 }
 
 // Karatsuba-style, 6 Fp2 products
-BGV_HD void fp6_mul(fp6_t& r, const fp6_t& a, const fp6_t& b) {
+BGV_NI void fp6_mul(fp6_t& r, const fp6_t& a, const fp6_t& b) {
   fp2_t t0, t1, t2, s0, s1, u;
   fp2_mul(t0, a.c0, b.c0);
   fp2_mul(t1, a.c1, b.c1);
@@ -68,7 +68,7 @@ BGV_HD void fp6_mul(fp6_t& r, const fp6_t& a, const fp6_t& b) {
 BGV_HD void fp6_sqr(fp6_t& r, const fp6_t& a) { fp6_mul(r, a, a); }
 
 // a * (b0 + b1 v): 5 Fp2 products
-BGV_HD void fp6_mul_01(fp6_t& r, const fp6_t& a, const fp2_t& b0, const fp2_t& b1) {
+BGV_NI void fp6_mul_01(fp6_t& r, const fp6_t& a, const fp2_t& b0, const fp2_t& b1) {
   fp2_t t0, t1, u, s0, s1, c0, c1, c2;
   fp2_mul(t0, a.c0, b0);
   fp2_mul(t1, a.c1, b1);
@@ -89,7 +89,7 @@ BGV_HD void fp6_mul_01(fp6_t& r, const fp6_t& a, const fp2_t& b0, const fp2_t& b
 }
 
 // a * (b1 v): 3 Fp2 products
-BGV_HD void fp6_mul_1(fp6_t& r, const fp6_t& a, const fp2_t& b1) {
+BGV_NI void fp6_mul_1(fp6_t& r, const fp6_t& a, const fp2_t& b1) {
   fp2_t c0, c1, c2;
   fp2_mul(c0, a.c2, b1);
   fp2_mul_xi(c0, c0);
@@ -98,7 +98,7 @@ BGV_HD void fp6_mul_1(fp6_t& r, const fp6_t& a, const fp2_t& b1) {
   r.c0 = c0; r.c1 = c1; r.c2 = c2;
 }
 
-BGV_HD void fp6_inv(fp6_t& r, const fp6_t& a) {
+BGV_NI void fp6_inv(fp6_t& r, const fp6_t& a) {
   // c0 = a0^2 - xi a1 a2, c1 = xi a2^2 - a0 a1, c2 = a1^2 - a0 a2
   fp2_t c0, c1, c2, t;
   fp2_sqr(c0, a.c0);
@@ -136,7 +136,7 @@ BGV_HD bool fp12_is_one(const fp12_t& a) {
 
 BGV_HD void fp12_conj(fp12_t& r, const fp12_t& a) { r.c0 = a.c0; fp6_neg(r.c1, a.c1); }
 
-BGV_HD void fp12_mul(fp12_t& r, const fp12_t& a, const fp12_t& b) {
+BGV_NI void fp12_mul(fp12_t& r, const fp12_t& a, const fp12_t& b) {
   fp6_t t0, t1, s0, s1;
   fp6_mul(t0, a.c0, b.c0);
   fp6_mul(t1, a.c1, b.c1);
@@ -150,7 +150,7 @@ BGV_HD void fp12_mul(fp12_t& r, const fp12_t& a, const fp12_t& b) {
 }
 
 // complex squaring: (a0 + a1 w)^2 = (a0^2 + v a1^2) + 2 a0 a1 w, 2 Fp6 products
-BGV_HD void fp12_sqr(fp12_t& r, const fp12_t& a) {
+BGV_NI void fp12_sqr(fp12_t& r, const fp12_t& a) {
   fp6_t t0, t1, t2;
   fp6_mul(t0, a.c0, a.c1);          // a0 a1
   fp6_add(t1, a.c0, a.c1);          // a0 + a1
@@ -164,7 +164,7 @@ BGV_HD void fp12_sqr(fp12_t& r, const fp12_t& a) {
 }
 
 // multiply by a sparse line  l = a0 + a1 w^2 + b1 w^3  (tower: c0 = (a0, a1, 0), c1 = (0, b1, 0))
-BGV_HD void fp12_mul_line(fp12_t& r, const fp12_t& f, const fp2_t& a0, const fp2_t& a1, const fp2_t& b1) {
+BGV_NI void fp12_mul_line(fp12_t& r, const fp12_t& f, const fp2_t& a0, const fp2_t& a1, const fp2_t& b1) {
   fp6_t t0, t1, s;
   fp6_mul_01(t0, f.c0, a0, a1);
   fp6_mul_1(t1, f.c1, b1);
@@ -178,7 +178,7 @@ BGV_HD void fp12_mul_line(fp12_t& r, const fp12_t& f, const fp2_t& a0, const fp2
   fp6_add(r.c0, t0, t1);
 }
 
-BGV_HD void fp12_inv(fp12_t& r, const fp12_t& a) {
+BGV_NI void fp12_inv(fp12_t& r, const fp12_t& a) {
   // 1 / (a0 + a1 w) = (a0 - a1 w) / (a0^2 - v a1^2)
   fp6_t t0, t1;
   fp6_sqr(t0, a.c0);
@@ -192,7 +192,7 @@ BGV_HD void fp12_inv(fp12_t& r, const fp12_t& a) {
 }
 
 // pi^k for k = 1, 2, 3: coefficient at w^i -> conj^k(c_i) * FROB_G[k-1][i-1]
-BGV_HD void fp12_frob(fp12_t& r, const fp12_t& a, int k) {
+BGV_NI void fp12_frob(fp12_t& r, const fp12_t& a, int k) {
   fp2_t c[6] = {a.c0.c0, a.c1.c0, a.c0.c1, a.c1.c1, a.c0.c2, a.c1.c2};
   if (k & 1) {
 #pragma unroll
@@ -204,7 +204,7 @@ BGV_HD void fp12_frob(fp12_t& r, const fp12_t& a, int k) {
 }
 
 // (a + b s)^2 in Fp4 = Fp2[s]/(s^2 - xi)
-BGV_HD void fp4_sqr(fp2_t& r0, fp2_t& r1, const fp2_t& a, const fp2_t& b) {
+BGV_NI void fp4_sqr(fp2_t& r0, fp2_t& r1, const fp2_t& a, const fp2_t& b) {
   fp2_t t0, t1, t2;
   fp2_sqr(t0, a);
   fp2_sqr(t1, b);
@@ -219,7 +219,7 @@ BGV_HD void fp4_sqr(fp2_t& r0, fp2_t& r1, const fp2_t& a, const fp2_t& b) {
 // Granger-Scott squaring, valid in the cyclotomic subgroup (after the easy part).
 // Fp12 viewed as Fp4[t]/(t^3 - s), s = w^3: A = c0 + c3 s, B = c1 + c4 s, C = c2 + c5 s.
 // A' = 3A^2 - 2 conj(A), B' = 3 s C^2 + 2 conj(B), C' = 3B^2 - 2 conj(C).
-BGV_HD void fp12_cyclotomic_sqr(fp12_t& r, const fp12_t& f) {
+BGV_NI void fp12_cyclotomic_sqr(fp12_t& r, const fp12_t& f) {
   fp2_t z0 = f.c0.c0, z1 = f.c1.c1;  // A
   fp2_t z2 = f.c1.c0, z3 = f.c0.c2;  // B
   fp2_t z4 = f.c0.c1, z5 = f.c1.c2;  // C
@@ -238,7 +238,7 @@ BGV_HD void fp12_cyclotomic_sqr(fp12_t& r, const fp12_t& f) {
 }
 
 // r = a^x for the (negative) BLS parameter x, a in the cyclotomic subgroup
-BGV_HD void fp12_pow_x(fp12_t& r, const fp12_t& a) {
+BGV_NI void fp12_pow_x(fp12_t& r, const fp12_t& a) {
   fp12_t acc = a;
   for (int b = 62; b >= 0; b--) {
     fp12_cyclotomic_sqr(acc, acc);
@@ -250,7 +250,7 @@ BGV_HD void fp12_pow_x(fp12_t& r, const fp12_t& a) {
 // f^((p^12 - 1) / r) up to the fixed cube: the hard part uses
 // 3 (p^4 - p^2 + 1) / r = (x - 1)^2 (x + p)(x^2 + p^2 - 1) + 3.
 // Equality with 1 is unaffected by the cube (gcd(3, r) = 1).
-BGV_HD void fp12_final_exp(fp12_t& r, const fp12_t& f) {
+BGV_NI void fp12_final_exp(fp12_t& r, const fp12_t& f) {
   fp12_t t0, t1, y0, y1, y2, y3;
   // easy part: f^((p^6 - 1)(p^2 + 1))
   fp12_inv(t0, f);

@@ -26,7 +26,7 @@ BGV_HD void fp2_mul4(fp2_t& r, const fp2_t& a) { fp_mul4(r.c0, a.c0); fp_mul4(r.
 BGV_HD void fp2_mul8(fp2_t& r, const fp2_t& a) { fp_mul8(r.c0, a.c0); fp_mul8(r.c1, a.c1); }
 
 // Karatsuba: 3 Fp products
-BGV_HD void fp2_mul(fp2_t& r, const fp2_t& a, const fp2_t& b) {
+BGV_NI void fp2_mul(fp2_t& r, const fp2_t& a, const fp2_t& b) {
   fp_t t0, t1, t2, t3;
   fp_mul(t0, a.c0, b.c0);
   fp_mul(t1, a.c1, b.c1);
@@ -39,7 +39,7 @@ BGV_HD void fp2_mul(fp2_t& r, const fp2_t& a, const fp2_t& b) {
 }
 
 // complex squaring: 2 Fp products
-BGV_HD void fp2_sqr(fp2_t& r, const fp2_t& a) {
+BGV_NI void fp2_sqr(fp2_t& r, const fp2_t& a) {
   fp_t t0, t1, t2;
   fp_add(t0, a.c0, a.c1);
   fp_sub(t1, a.c0, a.c1);
@@ -48,7 +48,7 @@ BGV_HD void fp2_sqr(fp2_t& r, const fp2_t& a) {
   fp_dbl(r.c1, t2);
 }
 
-BGV_HD void fp2_mul_fp(fp2_t& r, const fp2_t& a, const fp_t& b) { fp_mul(r.c0, a.c0, b); fp_mul(r.c1, a.c1, b); }
+BGV_NI void fp2_mul_fp(fp2_t& r, const fp2_t& a, const fp_t& b) { fp_mul(r.c0, a.c0, b); fp_mul(r.c1, a.c1, b); }
 
 // multiply by the tower non-residue xi = 1 + i
 BGV_HD void fp2_mul_xi(fp2_t& r, const fp2_t& a) {
@@ -67,7 +67,7 @@ BGV_HD void fp2_norm(fp_t& r, const fp2_t& a) {
   fp_add(r, t0, t1);
 }
 
-BGV_HD void fp2_inv(fp2_t& r, const fp2_t& a) {
+BGV_NI void fp2_inv(fp2_t& r, const fp2_t& a) {
   fp_t n, t;
   fp2_norm(n, a);
   fp_inv(n, n);
@@ -96,7 +96,7 @@ BGV_HD bool fp2_lex_largest(const fp2_t& a) {
 //   s^2 t == 1 :  x = s t + (a1 s / 2) i
 //   otherwise  :  x = (a1 s / 2) - (s t) i      (then -t is the square)
 // a1 == 0 is handled directly in Fp.  Returns false iff a is a non-square.
-BGV_HD bool fp2_sqrt(fp2_t& r, const fp2_t& a) {
+BGV_NI bool fp2_sqrt(fp2_t& r, const fp2_t& a) {
   if (fp_is_zero(a.c1)) {
     fp_t s;
     if (fp_sqrt(s, a.c0)) {
@@ -134,7 +134,7 @@ BGV_HD bool fp2_sqrt(fp2_t& r, const fp2_t& a) {
 }
 
 // a is a square in Fp2 iff its norm is a square in Fp
-BGV_HD bool fp2_is_square(const fp2_t& a) {
+BGV_NI bool fp2_is_square(const fp2_t& a) {
   fp_t n, l;
   fp2_norm(n, a);
   if (fp_is_zero(n)) return true;

@@ -33,7 +33,7 @@ BGV_CONST uint8_t DST_PRIME[44] = {'B', 'L', 'S', '_', 'S', 'I', 'G', '_', 'B', 
 BGV_HD uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 
 // one SHA-256 compression of a 16-word big-endian block
-BGV_HD void sha256_compress(uint32_t st[8], const uint32_t blk[16]) {
+BGV_NI void sha256_compress(uint32_t st[8], const uint32_t blk[16]) {
   uint32_t w[16];
 #pragma unroll
   for (int i = 0; i < 16; i++) w[i] = blk[i];
@@ -72,7 +72,7 @@ BGV_HD void blk_clear(uint32_t blk[16]) {
 }
 
 // expand_message_xmd(msg[32], DST, 256) -> 64 big-endian words
-BGV_HD void expand_message_xmd_256(uint32_t out[64], const uint8_t msg[32]) {
+BGV_NI void expand_message_xmd_256(uint32_t out[64], const uint8_t msg[32]) {
   uint32_t blk[16];
   uint32_t st[8];
   // b0 = H(Z_pad[64] || msg[32] || I2OSP(256, 2) || 0x00 || DST_prime[44]): 143 bytes, 3 blocks
@@ -146,7 +146,7 @@ BGV_HD void hash_to_field_fp2x2(fp2_t& u0, fp2_t& u1, const uint8_t msg[32]) {
 }
 
 // simplified SWU onto E2' (RFC 9380 6.6.2), affine output
-BGV_HD void map_to_curve_sswu(g2a& out, const fp2_t& u) {
+BGV_NI void map_to_curve_sswu(g2a& out, const fp2_t& u) {
   fp2_t u2, zu2, den, tv1, x1, x2, gx1, gx2, t;
   fp2_sqr(u2, u);
   fp2_mul(zu2, SSWU_Z, u2);
@@ -192,7 +192,7 @@ BGV_HD void fp2_horner(fp2_t& r, const fp2_t (&c)[N], const fp2_t& x) {
 
 // 3-isogeny E2' -> E2 straight into Jacobian coordinates (no inversion):
 // Z = xden yden, X = xnum xden yden^2, Y = y ynum xden^3 yden^2
-BGV_HD void iso_map_g2(g2j& r, const g2a& p) {
+BGV_NI void iso_map_g2(g2j& r, const g2a& p) {
   fp2_t xn, xd, yn, yd, t, yd2;
   fp2_horner(xn, ISO_XNUM, p.x);
   fp2_horner(xd, ISO_XDEN, p.x);
@@ -210,7 +210,7 @@ BGV_HD void iso_map_g2(g2j& r, const g2a& p) {
 }
 
 // full hash_to_G2(msg[32]) -> Jacobian point in G2
-BGV_HD void hash_to_g2(g2j& out, const uint8_t msg[32]) {
+BGV_NI void hash_to_g2(g2j& out, const uint8_t msg[32]) {
   fp2_t u0, u1;
   hash_to_field_fp2x2(u0, u1, msg);
   g2a q0a, q1a;

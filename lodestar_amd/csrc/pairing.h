@@ -13,7 +13,7 @@ namespace bgv {
 struct g2p_t { fp2_t x, y, z; };  // homogeneous projective: x = X/Z, y = Y/Z
 
 // T <- 2T, line tangent at T evaluated at P
-BGV_HD void miller_dbl_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const fp_t& xp, const fp_t& yp) {
+BGV_NI void miller_dbl_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const fp_t& xp, const fp_t& yp) {
   fp2_t A, B, C, E, F, G, H, t;
   fp2_mul(A, T.x, T.y);
   fp_half(A.c0, A.c0);
@@ -47,7 +47,7 @@ BGV_HD void miller_dbl_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const fp_
 }
 
 // T <- T + Q (Q affine), line through T and Q evaluated at P
-BGV_HD void miller_add_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const g2a& Q, const fp_t& xp,
+BGV_NI void miller_add_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const g2a& Q, const fp_t& xp,
                             const fp_t& yp) {
   fp2_t th, la, C, D, E, F, G, H, t;
   fp2_mul(t, Q.y, T.z);
@@ -80,7 +80,7 @@ BGV_HD void miller_add_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const g2a
 
 // f = f_{x, Q}(P) for the negative x (conjugated), P affine in G1, Q affine in G2.
 // P or Q at infinity gives 1.
-BGV_HD void miller_loop(fp12_t& f, const g1a& P, bool p_inf, const g2a& Q, bool q_inf) {
+BGV_NI void miller_loop(fp12_t& f, const g1a& P, bool p_inf, const g2a& Q, bool q_inf) {
   fp12_one(f);
   if (p_inf || q_inf) return;
   g2p_t T;

@@ -1,0 +1,253 @@
+"""ctypes binding of the C ABI in include/bgv.h (lodestar_amd/libbgv.so).
+
+This is the Python counterpart of the N-API addon described in
+INTEGRATION.md: plain pointers and sizes cross the boundary, nothing else.
+There is no CPU fallback: if the gfx950 library is missing or no HIP device
+is visible, every entry point raises ``BgvNativeError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libbgv.so")
+
+# include/bgv.h enums
+BGV_OK = 0
+BGV_E_INVALID_ARG = -1
+BGV_E_HIP = -2
+BGV_E_NO_DEVICE = -3
+BGV_E_TABLE_RANGE = -4
+BGV_E_EMPTY_SET = -5
+
+SET_CODE_NAMES = {
+    0: "BLST_SUCCESS",
+    1: "BLST_BAD_ENCODING",
+    2: "BLST_POINT_NOT_ON_CURVE",
+    3: "BLST_POINT_NOT_IN_GROUP",
+    4: "BLST_AGGR_TYPE_MISMATCH",
+    5: "BLST_VERIFY_FAIL",
+    6: "BLST_PK_IS_INFINITY",
+    7: "BLST_BAD_SCALAR",
+    8: "BLST_INVALID_SIZE",
+    9: "BGV_INDEX_RANGE",
+    10: "EMPTY_SIGNATURE_SET",
+}
+
+PK_COMPRESSED_48 = 0
+PK_UNCOMPRESSED_96 = 1
+N_STAGES = 10
+
+EXPORTS = [
+    "bgv_abi_version", "bgv_set_code_name", "bgv_stage_name", "bgv_last_error", "bgv_open", "bgv_close",
+    "bgv_pubkeys_set", "bgv_pubkeys_count", "bgv_pubkeys_get", "bgv_verify", "bgv_partial",
+    "bgv_combine_final", "bgv_gen_keys", "bgv_gen_sign", "bgv_bench_fpmul", "bgv_bench_mad",
+]
+
+
+class BgvNativeError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"bgv status {status}: {msg}")
+        self.status = status
+
+
+class BgvBatch(ctypes.Structure):
+    _fields_ = [
+        ("n_sets", ctypes.c_uint32),
+        ("n_jobs", ctypes.c_uint32),
+        ("job_offsets", ctypes.c_void_p),
+        ("pk_offsets", ctypes.c_void_p),
+        ("pk_indices", ctypes.c_void_p),
+        ("raw_pks", ctypes.c_void_p),
+        ("n_raw", ctypes.c_uint32),
+        ("msgs", ctypes.c_void_p),
+        ("sigs", ctypes.c_void_p),
+        ("sig_len", ctypes.c_void_p),
+        ("scalars", ctypes.c_void_p),
+        ("on_device", ctypes.c_uint32),
+    ]
+
+
+class BgvStats(ctypes.Structure):
+    _fields_ = [
+        ("stage_ms", ctypes.c_float * N_STAGES),
+        ("total_ms", ctypes.c_float),
+        ("batch_retries", ctypes.c_uint32),
+        ("batch_sigs_success", ctypes.c_uint32),
+        ("n_sets", ctypes.c_uint32),
+        ("n_jobs", ctypes.c_uint32),
+        ("pubkeys_aggregated", ctypes.c_uint64),
+    ]
+
+    def as_dict(self, lib=None):
+        names = [lib.stage_name(i) for i in range(N_STAGES)] if lib else [str(i) for i in range(N_STAGES)]
+        return {
+            "stage_ms": dict(zip(names, [float(x) for x in self.stage_ms])),
+            "total_ms": float(self.total_ms),
+            "batch_retries": int(self.batch_retries),
+            "batch_sigs_success": int(self.batch_sigs_success),
+            "n_sets": int(self.n_sets),
+            "n_jobs": int(self.n_jobs),
+            "pubkeys_aggregated": int(self.pubkeys_aggregated),
+        }
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libbgv.so (no compute). Raises BgvNativeError when absent."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise BgvNativeError(BGV_E_NO_DEVICE, f"{path} not built (run __graft_entry__.build())")
+        lib = ctypes.CDLL(path)
+        P = ctypes.c_void_p
+        u32, i32, u64 = ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64
+        sig = {
+            "bgv_abi_version": ([], ctypes.c_int),
+            "bgv_set_code_name": ([ctypes.c_int], ctypes.c_char_p),
+            "bgv_stage_name": ([ctypes.c_int], ctypes.c_char_p),
+            "bgv_last_error": ([], ctypes.c_char_p),
+            "bgv_open": ([ctypes.c_int, ctypes.POINTER(P)], ctypes.c_int),
+            "bgv_close": ([P], ctypes.c_int),
+            "bgv_pubkeys_set": ([P, u32, u32, P, u32], ctypes.c_int),
+            "bgv_pubkeys_count": ([P, ctypes.POINTER(u32)], ctypes.c_int),
+            "bgv_pubkeys_get": ([P, u32, u32, P], ctypes.c_int),
+            "bgv_verify": ([P, ctypes.POINTER(BgvBatch), P, P, ctypes.POINTER(BgvStats)], ctypes.c_int),
+            "bgv_partial": ([P, ctypes.POINTER(BgvBatch), P, P, ctypes.POINTER(i32)], ctypes.c_int),
+            "bgv_combine_final": ([P, P, u32, ctypes.POINTER(i32)], ctypes.c_int),
+            "bgv_gen_keys": ([P, u32, u32, u64], ctypes.c_int),
+            "bgv_gen_sign": ([P, ctypes.POINTER(BgvBatch), P], ctypes.c_int),
+            "bgv_bench_fpmul": ([P, u32, u32, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+            "bgv_bench_mad": ([P, u32, u32, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+        }
+        for name, (args, res) in sig.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = lib
+        return lib
+
+
+def _ptr(a) -> int | None:
+    """address of a numpy array / torch tensor / None"""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return int(a.data_ptr())  # torch tensor (device-resident)
+
+
+class Device:
+    """One bgv_ctx: a HIP device, its stream and its HBM pubkey table."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        self._check(self.lib.bgv_open(device, ctypes.byref(h)))
+        self.h = h
+        self.device = device
+        self.last_stats = BgvStats()
+
+    # -------------------------------------------------------------- helpers
+    def _check(self, st: int):
+        if st != BGV_OK:
+            raise BgvNativeError(st, self.lib.bgv_last_error().decode())
+
+    def stage_name(self, i: int) -> str:
+        return self.lib.bgv_stage_name(i).decode()
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.bgv_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------- pubkey table
+    def pubkeys_set(self, first: int, data: bytes | np.ndarray, fmt: int):
+        w = 48 if fmt == PK_COMPRESSED_48 else 96
+        arr = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else np.ascontiguousarray(data, dtype=np.uint8)
+        n = arr.size // w
+        self._check(self.lib.bgv_pubkeys_set(self.h, first, n, arr.ctypes.data, fmt))
+
+    def pubkeys_count(self) -> int:
+        c = ctypes.c_uint32()
+        self._check(self.lib.bgv_pubkeys_count(self.h, ctypes.byref(c)))
+        return c.value
+
+    def pubkeys_get(self, first: int, n: int) -> bytes:
+        out = np.zeros(n * 96, dtype=np.uint8)
+        self._check(self.lib.bgv_pubkeys_get(self.h, first, n, out.ctypes.data))
+        return out.tobytes()
+
+    def gen_keys(self, first: int, n: int, seed: int):
+        self._check(self.lib.bgv_gen_keys(self.h, first, n, seed))
+
+    # --------------------------------------------------------------- batches
+    @staticmethod
+    def make_batch(arrays: dict, on_device: bool = False) -> BgvBatch:
+        b = BgvBatch()
+        b.n_sets = int(arrays["n_sets"])
+        b.n_jobs = int(arrays["n_jobs"])
+        b.job_offsets = _ptr(arrays["job_offsets"])
+        b.pk_offsets = _ptr(arrays["pk_offsets"])
+        b.pk_indices = _ptr(arrays["pk_indices"])
+        b.raw_pks = _ptr(arrays.get("raw_pks"))
+        b.n_raw = int(arrays.get("n_raw", 0))
+        b.msgs = _ptr(arrays["msgs"])
+        b.sigs = _ptr(arrays.get("sigs"))
+        b.sig_len = _ptr(arrays.get("sig_len"))
+        b.scalars = _ptr(arrays.get("scalars"))
+        b.on_device = 1 if on_device else 0
+        return b
+
+    def verify(self, arrays: dict, on_device: bool = False, want_set_codes: bool = True):
+        """returns (job_result int32[n_jobs], set_code int32[n_sets] | None)"""
+        b = self.make_batch(arrays, on_device)
+        jr = np.zeros(max(b.n_jobs, 1), dtype=np.int32)
+        sc = np.zeros(max(b.n_sets, 1), dtype=np.int32) if want_set_codes else None
+        self._check(self.lib.bgv_verify(self.h, ctypes.byref(b), jr.ctypes.data,
+                                        sc.ctypes.data if sc is not None else None, ctypes.byref(self.last_stats)))
+        return jr[: b.n_jobs], (sc[: b.n_sets] if sc is not None else None)
+
+    def partial(self, arrays: dict, on_device: bool = False):
+        b = self.make_batch(arrays, on_device)
+        out = np.zeros(576, dtype=np.uint8)
+        sc = np.zeros(max(b.n_sets, 1), dtype=np.int32)
+        ok = ctypes.c_int32()
+        self._check(self.lib.bgv_partial(self.h, ctypes.byref(b), out.ctypes.data, sc.ctypes.data, ctypes.byref(ok)))
+        return out.tobytes(), sc[: b.n_sets], bool(ok.value)
+
+    def combine_final(self, partials: list[bytes]) -> bool:
+        buf = np.frombuffer(b"".join(partials), dtype=np.uint8) if partials else np.zeros(1, np.uint8)
+        r = ctypes.c_int32()
+        self._check(self.lib.bgv_combine_final(self.h, buf.ctypes.data, len(partials), ctypes.byref(r)))
+        return bool(r.value)
+
+    def gen_sign(self, arrays: dict, out, on_device: bool = False):
+        b = self.make_batch(arrays, on_device)
+        self._check(self.lib.bgv_gen_sign(self.h, ctypes.byref(b), _ptr(out)))
+
+    # ---------------------------------------------------------- microbench
+    def bench_fpmul(self, lanes: int, iters: int) -> float:
+        ms = ctypes.c_float()
+        self._check(self.lib.bgv_bench_fpmul(self.h, lanes, iters, ctypes.byref(ms)))
+        return ms.value
+
+    def bench_mad(self, lanes: int, iters: int) -> float:
+        ms = ctypes.c_float()
+        self._check(self.lib.bgv_bench_mad(self.h, lanes, iters, ctypes.byref(ms)))
+        return ms.value

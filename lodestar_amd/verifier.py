@@ -1,0 +1,436 @@
+"""Host-side mirror of Lodestar's BLS verifier interface, backed by the gfx950
+HIP library through the C ABI (lodestar_amd/native.py -> include/bgv.h).
+
+Reference interface (maschad/lodestar, packages/beacon-node/src/chain/bls/):
+
+* ``IBlsVerifier`` (interface.ts:20-51): ``verifySignatureSets(sets, opts)``
+  -> Promise<boolean>, ``close()``, ``canAcceptWork()``.  Here:
+  ``BlsGpuVerifier.verify_signature_sets`` (a coroutine), ``close``,
+  ``can_accept_work``.
+* ``VerifySignatureOpts`` {batchable, verifyOnMainThread} (interface.ts:3-18).
+* ``ISignatureSet`` single / aggregate (state-transition/src/util/
+  signatureSets.ts:5-22).  Pubkeys are references into the HBM-resident
+  ``index2pubkey`` table (``PubkeyTable``), so a set carries index lists
+  instead of serialized points (BASELINE north_star); raw pubkeys outside
+  the table are still accepted (``PublicKey.from_bytes``).
+* Pool semantics of ``BlsMultiThreadWorkerPool`` (multithread/index.ts:
+  151-431): sets chunked into jobs of <= 128 (``chunkify_maximize_chunk_size``,
+  multithread/utils.ts:4-19), batchable jobs buffered up to 100 ms or until
+  more than 32 sigs are waiting, job verdict = AND of its sets, the call's
+  verdict = AND of its jobs, a job whose signature does not parse rejects
+  with ``BLST_ERROR: BLST_<CODE>``, an empty aggregate rejects with
+  ``EMPTY_AGGREGATE_ARRAY``, a job of zero sets rejects with
+  ``Empty signature set`` (maybeBatch.ts:29-31), ``close()`` rejects pending
+  jobs with ``QueueError(QUEUE_ABORTED)`` (multithread/index.ts:193-214).
+
+What differs on purpose: the worker pool packs <= 128 sigs per worker
+message (prepareWork, index.ts:405-420) because a CPU worker verifies one
+batch at a time; a GPU wants one large batch, so every queued job is packed
+into one device batch (bounded by ``max_sets_per_device_batch``).  Verdicts
+are unaffected: the device checks the whole batch once and falls back to
+per-job checks exactly where the worker retries (worker.ts:64-85).
+"""
+from __future__ import annotations
+
+import asyncio
+import enum
+import math
+import os
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import native
+
+MAX_SIGNATURE_SETS_PER_JOB = 128  # multithread/index.ts:39
+MAX_BUFFERED_SIGS = 32            # multithread/index.ts:48
+MAX_BUFFER_WAIT_MS = 100          # multithread/index.ts:57
+MAX_JOBS_CAN_ACCEPT_WORK = 512    # multithread/index.ts:62
+MAX_SETS_PER_DEVICE_BATCH = 1 << 17
+
+
+class BlsError(Exception):
+    """Rejection raised by verify_signature_sets; ``message`` follows the
+    strings the reference's tests match (multithread.test.ts:97,
+    test/spec/general/bls.ts:37)."""
+
+    def __init__(self, message: str, code: int | None = None):
+        super().__init__(message)
+        self.message = message
+        self.code = code
+
+
+class QueueErrorCode(str, enum.Enum):
+    QUEUE_ABORTED = "QUEUE_ERROR_QUEUE_ABORTED"  # util/queue/errors.ts
+
+
+class QueueError(Exception):
+    def __init__(self, code: QueueErrorCode = QueueErrorCode.QUEUE_ABORTED):
+        super().__init__(code.value)
+        self.code = code
+
+
+def error_for_code(code: int) -> BlsError:
+    if code == 10:
+        return BlsError("Empty signature set", code)
+    return BlsError(f"BLST_ERROR: {native.SET_CODE_NAMES.get(code, 'BLST_UNKNOWN')}", code)
+
+
+# --------------------------------------------------------------- data types
+class SignatureSetType(str, enum.Enum):
+    single = "single"
+    aggregate = "aggregate"
+
+
+@dataclass(frozen=True)
+class PublicKey:
+    """A trusted pubkey: either a row of the device index2pubkey table
+    (``index``) or raw bytes (96 B uncompressed x||y, or 48 B compressed)."""
+
+    index: int | None = None
+    raw: bytes | None = None
+
+    @staticmethod
+    def from_bytes(b: bytes) -> "PublicKey":
+        if len(b) not in (48, 96):
+            raise BlsError("BLST_ERROR: BLST_INVALID_SIZE", 8)
+        return PublicKey(raw=bytes(b))
+
+
+@dataclass
+class VerifySignatureOpts:
+    batchable: bool = False
+    verifyOnMainThread: bool = False
+
+
+@dataclass
+class ISignatureSet:
+    type: SignatureSetType
+    signingRoot: bytes
+    signature: bytes
+    pubkey: PublicKey | None = None
+    pubkeys: list[PublicKey] = field(default_factory=list)
+
+
+def create_single_signature_set_from_components(pubkey: PublicKey, signing_root: bytes, signature: bytes) -> ISignatureSet:
+    """util/signatureSets.ts:40-51"""
+    return ISignatureSet(SignatureSetType.single, bytes(signing_root), bytes(signature), pubkey=pubkey)
+
+
+def create_aggregate_signature_set_from_components(pubkeys, signing_root: bytes, signature: bytes) -> ISignatureSet:
+    """util/signatureSets.ts:53-64"""
+    return ISignatureSet(SignatureSetType.aggregate, bytes(signing_root), bytes(signature), pubkeys=list(pubkeys))
+
+
+def get_aggregated_pubkeys_count(sets) -> int:
+    """chain/bls/utils.ts:18-26"""
+    return sum(len(s.pubkeys) for s in sets if s.type == SignatureSetType.aggregate)
+
+
+def chunkify_maximize_chunk_size(arr: list, min_per_chunk: int) -> list[list]:
+    """multithread/utils.ts:4-19: split maximizing the smallest chunk."""
+    chunk_count = len(arr) // min_per_chunk
+    if chunk_count <= 1:
+        return [arr]
+    per_chunk = math.ceil(len(arr) / chunk_count)
+    return [arr[i : i + per_chunk] for i in range(0, len(arr), per_chunk)]
+
+
+# ------------------------------------------------------------ pubkey table
+class PubkeyTable:
+    """``index2pubkey`` resident in HBM (state-transition/src/cache/
+    pubkeyCache.ts:6,56-77 syncPubkeys; cache/epochContext.ts:701-704
+    addPubkey).  One replica per device."""
+
+    def __init__(self, devices: list[native.Device]):
+        self.devices = devices
+        self.pubkey2index: dict[bytes, int] = {}
+
+    def __len__(self):
+        return self.devices[0].pubkeys_count()
+
+    def sync_pubkeys(self, pubkeys48: list[bytes]):
+        """Append every validator pubkey not yet in the table (compressed)."""
+        start = len(self)
+        new = pubkeys48[start:]
+        if not new:
+            return
+        blob = b"".join(new)
+        for d in self.devices:
+            d.pubkeys_set(start, blob, native.PK_COMPRESSED_48)
+        for i, pk in enumerate(new):
+            self.pubkey2index[bytes(pk)] = start + i
+
+    def add_pubkey(self, index: int, pubkey48: bytes):
+        for d in self.devices:
+            d.pubkeys_set(index, pubkey48, native.PK_COMPRESSED_48)
+        self.pubkey2index[bytes(pubkey48)] = index
+
+    def __getitem__(self, index: int) -> PublicKey:
+        return PublicKey(index=index)
+
+
+# ------------------------------------------------------- batch marshalling
+def encode_jobs(jobs: list[list[ISignatureSet]], scalars: np.ndarray | None = None) -> dict:
+    """Flatten jobs of sets into the SoA arrays of bgv_batch (include/bgv.h).
+    Raises BlsError("EMPTY_AGGREGATE_ARRAY") like PublicKey.aggregate."""
+    job_off = [0]
+    pk_off = [0]
+    idx: list[int] = []
+    raw: list[bytes] = []
+    raw_pos: dict[bytes, int] = {}
+    n = sum(len(j) for j in jobs)
+    msgs = np.zeros((max(n, 1), 32), dtype=np.uint8)
+    sigs = np.zeros((max(n, 1), 192), dtype=np.uint8)
+    sig_len = np.zeros(max(n, 1), dtype=np.uint32)
+    i = 0
+    for job in jobs:
+        for s in job:
+            pks = [s.pubkey] if s.type == SignatureSetType.single else s.pubkeys
+            if len(pks) == 0:
+                raise BlsError("EMPTY_AGGREGATE_ARRAY")
+            for pk in pks:
+                if pk.index is not None:
+                    idx.append(pk.index)
+                else:
+                    r = pk.raw if len(pk.raw) == 96 else _decompress_raw48(pk.raw)
+                    if r not in raw_pos:
+                        raw_pos[r] = len(raw)
+                        raw.append(r)
+                    idx.append(0x80000000 | raw_pos[r])
+            pk_off.append(len(idx))
+            if len(s.signingRoot) != 32:
+                raise BlsError("signingRoot must be 32 bytes")
+            msgs[i] = np.frombuffer(s.signingRoot, dtype=np.uint8)
+            sl = len(s.signature)
+            sig_len[i] = sl
+            if sl in (96, 192):
+                sigs[i, :sl] = np.frombuffer(s.signature, dtype=np.uint8)
+            i += 1
+        job_off.append(i)
+    out = {
+        "n_sets": n,
+        "n_jobs": len(jobs),
+        "job_offsets": np.array(job_off, dtype=np.uint32),
+        "pk_offsets": np.array(pk_off, dtype=np.uint32),
+        "pk_indices": np.array(idx if idx else [0], dtype=np.uint32),
+        "raw_pks": np.frombuffer(b"".join(raw), dtype=np.uint8).copy() if raw else None,
+        "n_raw": len(raw),
+        "msgs": msgs,
+        "sigs": sigs,
+        "sig_len": sig_len,
+        "scalars": scalars,
+    }
+    return out
+
+
+def _decompress_raw48(b: bytes) -> bytes:
+    raise BlsError("raw compressed pubkeys must be added to the table (PubkeyTable.add_pubkey)")
+
+
+# ----------------------------------------------------------------- verifier
+@dataclass
+class _Job:
+    sets: list
+    opts: VerifySignatureOpts
+    future: asyncio.Future
+    added: float
+
+
+class BlsGpuVerifier:
+    """``IBlsVerifier`` on one or more MI355X devices.
+
+    devices: HIP device ordinals.  Jobs of one device batch are split by job
+    across devices (each device holds a replica of the pubkey table)."""
+
+    def __init__(self, devices=(0,), metrics: dict | None = None, scalar_seed: int | None = None,
+                 max_sets_per_device_batch: int = MAX_SETS_PER_DEVICE_BATCH):
+        self.devices = [native.Device(d) for d in devices]
+        self.table = PubkeyTable(self.devices)
+        self.metrics = metrics if metrics is not None else _new_metrics()
+        self._rng = np.random.default_rng(scalar_seed) if scalar_seed is not None else None
+        self._max_batch = max_sets_per_device_batch
+        self._jobs: list[_Job] = []
+        self._buffered: list[_Job] = []
+        self._buffered_sigs = 0
+        self._buffer_handle = None
+        self._closed = False
+        self._busy = 0
+        self._exec = ThreadPoolExecutor(max_workers=len(self.devices))
+        self._dev_locks = [threading.Lock() for _ in self.devices]
+
+    # -- IBlsVerifier ---------------------------------------------------
+    def can_accept_work(self) -> bool:
+        """multithread/index.ts:143-149 (device count stands in for workers)"""
+        return self._busy < len(self.devices) and len(self._jobs) < MAX_JOBS_CAN_ACCEPT_WORK
+
+    async def verify_signature_sets(self, sets: list[ISignatureSet], opts: VerifySignatureOpts | None = None) -> bool:
+        opts = opts or VerifySignatureOpts()
+        self.metrics["aggregated_pubkeys_total"] += get_aggregated_pubkeys_count(sets)
+        for s in sets:  # PublicKey.aggregate throws on the main thread (utils.ts:11)
+            if s.type == SignatureSetType.aggregate and len(s.pubkeys) == 0:
+                raise BlsError("EMPTY_AGGREGATE_ARRAY")
+        if opts.verifyOnMainThread:
+            # unbuffered, high priority: one device batch right now
+            res = await asyncio.get_running_loop().run_in_executor(self._exec, self._run_device_batch, [sets])
+            r = res[0]
+            if isinstance(r, Exception):
+                raise r
+            return r
+        chunks = chunkify_maximize_chunk_size(sets, MAX_SIGNATURE_SETS_PER_JOB)
+        results = await asyncio.gather(*[self._queue_work(c, opts) for c in chunks])
+        if len(results) == 0:
+            raise BlsError("Empty results array")
+        return all(r is True for r in results)
+
+    async def close(self):
+        self._closed = True
+        if self._buffer_handle is not None:
+            self._buffer_handle.cancel()
+            self._buffer_handle = None
+        for j in self._jobs + self._buffered:
+            if not j.future.done():
+                j.future.set_exception(QueueError(QueueErrorCode.QUEUE_ABORTED))
+        self._jobs.clear()
+        self._buffered.clear()
+        self._exec.shutdown(wait=True)
+        for d in self.devices:
+            d.close()
+
+    # -- synchronous helpers ------------------------------------------------
+    def verify_signature_sets_maybe_batch(self, sets: list[ISignatureSet]) -> bool:
+        """maybeBatch.ts:16-38 for one job, synchronously (BlsSingleThreadVerifier
+        path, singleThread.ts:14-35)."""
+        r = self._run_device_batch([sets])[0]
+        if isinstance(r, Exception):
+            raise r
+        return r
+
+    # -- queueing -------------------------------------------------------------
+    async def _queue_work(self, sets, opts) -> bool:
+        if self._closed:
+            raise QueueError(QueueErrorCode.QUEUE_ABORTED)
+        loop = asyncio.get_running_loop()
+        job = _Job(sets, opts, loop.create_future(), time.monotonic())
+        if opts.batchable:
+            if not self._buffered:
+                self._buffer_handle = loop.call_later(MAX_BUFFER_WAIT_MS / 1000, self._run_buffered)
+            self._buffered.append(job)
+            self._buffered_sigs += len(sets)
+            if self._buffered_sigs > MAX_BUFFERED_SIGS:
+                self._buffer_handle.cancel()
+                self._run_buffered()
+        else:
+            self._jobs.append(job)
+            loop.call_soon(self._schedule)
+        return await job.future
+
+    def _run_buffered(self):
+        self._jobs.extend(self._buffered)
+        self._buffered = []
+        self._buffered_sigs = 0
+        self._buffer_handle = None
+        asyncio.get_running_loop().call_soon(self._schedule)
+
+    def _schedule(self):
+        if self._closed or not self._jobs or self._busy >= 1:
+            return
+        take, n = [], 0
+        while self._jobs and (n == 0 or n + len(self._jobs[0].sets) <= self._max_batch):
+            j = self._jobs.pop(0)
+            take.append(j)
+            n += len(j.sets)
+        self._busy += 1
+        asyncio.ensure_future(self._run(take))
+
+    async def _run(self, jobs: list[_Job]):
+        loop = asyncio.get_running_loop()
+        try:
+            now = time.monotonic()
+            for j in jobs:
+                self.metrics["job_wait_time_s"].append(now - j.added)
+            results = await loop.run_in_executor(self._exec, self._run_device_batch, [j.sets for j in jobs])
+            for j, r in zip(jobs, results):
+                if j.future.done():
+                    continue
+                if isinstance(r, Exception):
+                    j.future.set_exception(r)
+                else:
+                    j.future.set_result(r)
+        except Exception as e:  # device failure rejects the whole package (index.ts:386-393)
+            for j in jobs:
+                if not j.future.done():
+                    j.future.set_exception(e)
+        finally:
+            self._busy -= 1
+            loop.call_soon(self._schedule)
+
+    # -- device -------------------------------------------------------------
+    def _scalars(self, n: int) -> np.ndarray | None:
+        if self._rng is None:
+            return None  # getrandom() inside the library
+        s = self._rng.integers(1, 2**64 - 1, size=max(n, 1), dtype=np.uint64, endpoint=True)
+        return s
+
+    def _run_device_batch(self, jobs: list[list[ISignatureSet]]) -> list:
+        """Verify a list of jobs; returns per job True / False / BlsError."""
+        if not jobs:
+            return []
+        # shard whole jobs across devices, balanced by set count
+        nd = len(self.devices)
+        shards: list[list[int]] = [[] for _ in range(nd)]
+        load = [0] * nd
+        for k in sorted(range(len(jobs)), key=lambda k: -len(jobs[k])):
+            d = load.index(min(load))
+            shards[d].append(k)
+            load[d] += max(len(jobs[k]), 1)
+        out: list = [None] * len(jobs)
+
+        def run_shard(d: int):
+            ids = sorted(shards[d])
+            if not ids:
+                return
+            sub = [jobs[k] for k in ids]
+            try:
+                arrays = encode_jobs(sub, self._scalars(sum(len(j) for j in sub)))
+            except BlsError as e:
+                for k in ids:
+                    out[k] = e
+                return
+            with self._dev_locks[d]:
+                t0 = time.perf_counter()
+                jr, _ = self.devices[d].verify(arrays, want_set_codes=False)
+                st = self.devices[d].last_stats
+                self.metrics["batch_retries"] += int(st.batch_retries)
+                self.metrics["batch_sigs_success"] += int(st.batch_sigs_success)
+                self.metrics["device_time_s"] += time.perf_counter() - t0
+            for k, r in zip(ids, jr.tolist()):
+                out[k] = True if r == 1 else False if r == 0 else error_for_code(-r)
+
+        if nd == 1:
+            run_shard(0)
+        else:
+            ths = [threading.Thread(target=run_shard, args=(d,)) for d in range(nd)]
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+        self.metrics["sets_started"] += sum(len(j) for j in jobs)
+        self.metrics["jobs_started"] += len(jobs)
+        return out
+
+
+def _new_metrics() -> dict:
+    """Counterparts of lodestar_bls_thread_pool_* (metrics/metrics/lodestar.ts:350-430)."""
+    return {
+        "aggregated_pubkeys_total": 0,
+        "jobs_started": 0,
+        "sets_started": 0,
+        "batch_retries": 0,
+        "batch_sigs_success": 0,
+        "device_time_s": 0.0,
+        "job_wait_time_s": [],
+    }

@@ -880,3 +880,29 @@ def batch_verify(sets, scalars) -> bool:
 def interop_secret_key(index: int) -> int:
     d = hashlib.sha256(index.to_bytes(32, "little")).digest()
     return int.from_bytes(d, "little") % R
+
+
+# --------------------------------------------------------------------------
+# Job semantics of the reference pool (maybeBatch.ts:16-38)
+# --------------------------------------------------------------------------
+
+
+def verify_job(sets, scalars=None):
+    """``verifySignatureSetsMaybeBatch`` for one job.
+
+    sets: list of (pk_point_or_None, msg32, sig_bytes); pk already aggregated.
+    Every signature is parsed + subgroup-checked first (``sets.map(fromBytes)``,
+    maybeBatch.ts:20-24), raising BlstError on the first failure in set
+    order.  n >= 2: random-scalar batch verify (``scalars`` injected);
+    n == 1: core verify; n == 0: ValueError("Empty signature set").
+    Returns the boolean verdict."""
+    if len(sets) == 0:
+        raise ValueError("Empty signature set")
+    parsed = [(pk, msg, signature_from_bytes(sig, True)) for pk, msg, sig in sets]
+    for pk, _, _ in parsed:
+        if pk is None:
+            raise BlstError(BLST_PK_IS_INFINITY)
+    if len(parsed) >= 2:
+        return batch_verify(parsed, scalars if scalars is not None else [1 + i for i in range(len(parsed))])
+    pk, msg, sig = parsed[0]
+    return core_verify(pk, msg, sig)

@@ -1,0 +1,185 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle's
+golden vectors and against oracle-computed values.  Run on an MI355X:
+
+    python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+"""
+import asyncio
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import bls12_381 as B
+from tests import gpu_util as G
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from lodestar_amd import native
+    d = native.Device(0)
+    d.pubkeys_set(0, G.interop_pubkeys48(), native.PK_COMPRESSED_48)
+    yield d
+    d.close()
+
+
+def test_table_decompression_matches_oracle(dev):
+    """bgv_pubkeys_set(compressed) == oracle g1_decompress for all 100 interop keys."""
+    pks = G.interop_pubkeys48()
+    got = dev.pubkeys_get(0, 100)
+    for i in range(100):
+        code, pt = B.g1_decompress(pks[48 * i : 48 * i + 48])
+        assert code == 0
+        assert got[96 * i : 96 * i + 96] == B.g1_serialize(pt), i
+
+
+def test_golden_batch_all_jobs(dev):
+    arrays, expected, codes = G.golden_arrays()
+    jr, sc = dev.verify(arrays)
+    assert jr.tolist() == expected
+    assert sc.tolist() == codes
+    st = dev.last_stats
+    assert st.batch_retries == 1  # the batch holds invalid jobs
+
+
+@pytest.mark.parametrize("job", list(range(16)))
+def test_golden_each_job_alone(dev, job):
+    arrays, expected, codes = G.golden_arrays([job])
+    jr, sc = dev.verify(arrays)
+    assert jr.tolist() == expected
+    assert sc.tolist() == codes
+
+
+def test_golden_valid_jobs_single_batch_check(dev):
+    valid = [0, 1, 9, 11, 12, 13]
+    arrays, expected, _ = G.golden_arrays(valid)
+    jr, _ = dev.verify(arrays)
+    assert jr.tolist() == [1] * len(valid) == expected
+    assert dev.last_stats.batch_retries == 0
+    assert dev.last_stats.batch_sigs_success == arrays["n_sets"]
+
+
+def test_verdict_independent_of_scalars(dev):
+    for seed in (1, 2, 3):
+        arrays, expected, _ = G.golden_arrays(scalars_seed=seed)
+        jr, _ = dev.verify(arrays)
+        assert jr.tolist() == expected
+    arrays, expected, _ = G.golden_arrays()
+    arrays["scalars"] = None  # getrandom() inside the library
+    jr, _ = dev.verify(arrays)
+    assert jr.tolist() == expected
+
+
+def test_partial_combine_matches_verify(dev):
+    valid = [0, 1, 9, 11]
+    a0, _, _ = G.golden_arrays(valid[:2])
+    a1, _, _ = G.golden_arrays(valid[2:])
+    p0, _, ok0 = dev.partial(a0)
+    p1, _, ok1 = dev.partial(a1)
+    assert ok0 and ok1
+    assert dev.combine_final([p0, p1])
+    bad, _, _ = G.golden_arrays([2])  # wrong-message job
+    p2, _, ok2 = dev.partial(bad)
+    assert ok2
+    assert not dev.combine_final([p0, p1, p2])
+
+
+def test_gen_keys_and_sign_match_oracle(dev):
+    from lodestar_amd import native
+    d = native.Device(0)
+    seed = 0x4C4F4445
+    d.gen_keys(0, 8, seed)
+    got = d.pubkeys_get(0, 8)
+    for i in range(8):
+        h = hashlib.sha256(b"bgv-sk" + seed.to_bytes(8, "little") + i.to_bytes(4, "little")).digest()
+        sk = int.from_bytes(h, "big") % B.R
+        assert got[96 * i : 96 * i + 96] == B.g1_serialize(B.sk_to_pk(sk)), i
+    # one aggregate set over keys 1, 3, 5 signed on the device
+    m = hashlib.sha256(b"m").digest()
+    arrays = {"n_sets": 1, "n_jobs": 1, "job_offsets": np.array([0, 1], np.uint32),
+              "pk_offsets": np.array([0, 3], np.uint32), "pk_indices": np.array([1, 3, 5], np.uint32),
+              "msgs": np.frombuffer(m, np.uint8).copy()}
+    out = np.zeros(192, np.uint8)
+    d.gen_sign(arrays, out)
+    sks = [int.from_bytes(hashlib.sha256(b"bgv-sk" + seed.to_bytes(8, "little") + i.to_bytes(4, "little")).digest(), "big") % B.R for i in (1, 3, 5)]
+    assert out[:96].tobytes() == B.g2_compress(B.sign(sum(sks) % B.R, m))
+    d.close()
+
+
+def _synthetic(dev_, n_sets, k, n_keys, seed, fault_every=0):
+    """device-generated keys + signatures; every fault_every-th set signs the wrong message"""
+    rng = np.random.default_rng(seed)
+    idx = np.concatenate([rng.choice(n_keys, size=k, replace=False) for _ in range(n_sets)]).astype(np.uint32)
+    msgs = rng.integers(0, 256, size=(n_sets, 32), dtype=np.uint8)
+    arrays = {"n_sets": n_sets, "n_jobs": n_sets, "job_offsets": np.arange(n_sets + 1, dtype=np.uint32),
+              "pk_offsets": (np.arange(n_sets + 1) * k).astype(np.uint32), "pk_indices": idx, "msgs": msgs}
+    sigs = np.zeros((n_sets, 192), np.uint8)
+    sign_msgs = msgs.copy()
+    bad = np.zeros(n_sets, bool)
+    if fault_every:
+        bad[::fault_every] = True
+        sign_msgs[bad, 0] ^= 1
+    dev_.gen_sign(dict(arrays, msgs=sign_msgs), sigs)
+    arrays["sigs"] = sigs
+    arrays["sig_len"] = np.full(n_sets, 96, np.uint32)
+    arrays["scalars"] = rng.integers(1, 2**63, size=n_sets, dtype=np.uint64)
+    return arrays, bad
+
+
+def test_synthetic_batch_with_faults():
+    from lodestar_amd import native
+    d = native.Device(0)
+    d.gen_keys(0, 512, 99)
+    arrays, bad = _synthetic(d, 300, 16, 512, 5, fault_every=37)
+    jr, sc = d.verify(arrays)
+    assert (jr == np.where(bad, 0, 1)).all()
+    assert (sc == 0).all()
+    # the same sets grouped as 3 jobs of 100: a job is valid iff it has no fault
+    arrays["n_jobs"] = 3
+    arrays["job_offsets"] = np.array([0, 100, 200, 300], np.uint32)
+    jr, _ = d.verify(arrays)
+    assert jr.tolist() == [int(not bad[i * 100 : (i + 1) * 100].any()) for i in range(3)]
+    d.close()
+
+
+def test_async_verifier_like_reference_e2e():
+    """packages/beacon-node/test/e2e/chain/bls/multithread.test.ts:8-104 on the GPU:
+    three valid single sets (sk = 0x0101.., 0x0202.., 0x0303.., msg = same bytes)
+    resolve true whether submitted sync / async / batchable; a 32-byte signature
+    in a batchable job rejects with BLST_INVALID_SIZE while 8 others resolve true."""
+    from lodestar_amd import verifier as V
+    v = G.batch_vectors()
+    sets = []
+    for k in range(3):
+        s = v["jobs"][0]["sets"][k]
+        pk = V.PublicKey.from_bytes(bytes.fromhex(v["raw_pubkeys"][k]))
+        sets.append(V.create_single_signature_set_from_components(pk, bytes.fromhex(s["msg"]), bytes.fromhex(s["sig"])))
+
+    async def run():
+        pool = V.BlsGpuVerifier(devices=(0,))
+        try:
+            assert await pool.verify_signature_sets(sets)
+            assert await pool.verify_signature_sets(sets, V.VerifySignatureOpts(batchable=True))
+            assert await pool.verify_signature_sets(sets, V.VerifySignatureOpts(verifyOnMainThread=True))
+            good = [pool.verify_signature_sets(sets, V.VerifySignatureOpts(batchable=True)) for _ in range(8)]
+            bad_set = V.create_single_signature_set_from_components(sets[0].pubkey, sets[0].signingRoot, bytes(32))
+            bad = pool.verify_signature_sets([bad_set], V.VerifySignatureOpts(batchable=True))
+            res = await asyncio.gather(*good, bad, return_exceptions=True)
+            assert res[:8] == [True] * 8
+            assert isinstance(res[8], V.BlsError) and "BLST_INVALID_SIZE" in str(res[8])
+            with pytest.raises(V.BlsError, match="Empty signature set"):
+                await pool.verify_signature_sets([])
+            with pytest.raises(V.BlsError, match="EMPTY_AGGREGATE_ARRAY"):
+                await pool.verify_signature_sets([V.create_aggregate_signature_set_from_components([], bytes(32), bytes(96))])
+        finally:
+            await pool.close()
+        with pytest.raises(V.QueueError):
+            await pool.verify_signature_sets(sets)
+
+    asyncio.run(run())
+
+
+def test_microbench_runs(dev):
+    assert dev.bench_fpmul(256 * 64, 64) > 0
+    assert dev.bench_mad(256 * 64, 64) > 0

@@ -1,0 +1,56 @@
+"""Build the gfx950 shared library lodestar_amd/libbgv.so in-tree.
+
+hipcc compiles the kernels and the C-ABI host code (both .hip translation
+units) for gfx950 only.  Incremental: rebuilds when any source is newer than
+the library.  Used by __graft_entry__.build() and the test suite."""
+import glob
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "lodestar_amd", "csrc")
+LIB = os.path.join(ROOT, "lodestar_amd", "libbgv.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+SOURCES = ["bgv_kernels.hip", "bgv_api.hip"]
+
+
+def deps():
+    return (glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.hip"))
+            + [os.path.join(ROOT, "include", "bgv.h"), os.path.abspath(__file__)])
+
+
+def stale(lib=LIB):
+    if not os.path.exists(lib):
+        return True
+    t = os.path.getmtime(lib)
+    return any(os.path.getmtime(d) > t for d in deps())
+
+
+def build(force=False, verbose=False):
+    if not force and not stale():
+        return LIB
+    objs = []
+    procs = []
+    for s in SOURCES:
+        o = os.path.join(CSRC, s.replace(".hip", ".o"))
+        cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+               "-I" + os.path.join(ROOT, "include"), "-c", os.path.join(CSRC, s), "-o", o]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        procs.append(subprocess.Popen(cmd))
+        objs.append(o)
+    for p in procs:
+        if p.wait() != 0:
+            raise RuntimeError("hipcc failed")
+    tmp = LIB + ".tmp"
+    subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs)
+    os.replace(tmp, LIB)
+    for o in objs:
+        os.remove(o)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)
+    print(LIB)
