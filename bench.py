@@ -1,0 +1,246 @@
+"""Benchmark: BLS signature sets verified per second on MI355X.
+
+Workload (BASELINE.json configs[3], "C4"): a 32-epoch range-sync chain
+segment = 1024 blocks x 98 signature sets (95 attestation aggregates of 128
+pubkeys + 1 sync aggregate of 512 + randao + proposer singles) = 100,352
+sets, 12.98 M pubkey references into a 1,048,576-validator index2pubkey
+table resident in HBM.  One block = one verifySignatureSets call = one job
+(verifyBlocksSignatures.ts:30-47; non-batchable, <= 128 sets per job).
+
+A step = one pass of the hot path over the whole segment: every set's
+signature decoded + subgroup-checked, every message hashed to G2, every
+pubkey set gathered and aggregated from the table, 64-bit random scalars
+drawn (getrandom) and applied, one Miller loop per set, per-block products,
+and the final exponentiation (one for the segment; per-block ones only if
+it fails).  Inputs (indices, messages, signatures) are resident in HBM
+before the timed region.  Multi-GPU: blocks are split across ranks (strong
+scaling of the fixed segment); each rank reduces its shard to one Fp12
+Miller product, the 576-byte partials are all-gathered over RCCL and every
+rank runs the single final exponentiation on their product.
+
+Synthetic data: keys sk_i = SHA256("bgv-sk"||LE64(seed)||LE32(i)) mod r and
+signatures are generated on the device (bgv_gen_keys / bgv_gen_sign).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--blocks B]
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+N_VALIDATORS = 1 << 20
+SETS_PER_BLOCK = 98
+ATT_PER_BLOCK = 95
+ATT_K = 128
+SYNC_K = 512
+SEED = 0x4C4F4445
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def build_segment(blocks: list[int], seed: int = SEED):
+    """Host arrays for the given block ids of the segment (deterministic per block)."""
+    job_off, pk_off, idx, msgs = [0], [0], [], []
+    perm = np.random.default_rng(seed).permutation(N_VALIDATORS).astype(np.uint32)
+    n = 0
+    for b in blocks:
+        rng = np.random.default_rng([seed, b])
+        # attesters of the block: disjoint committees (a slice of a shuffling)
+        start = int(rng.integers(0, N_VALIDATORS))
+        att = np.take(perm, np.arange(start, start + ATT_PER_BLOCK * ATT_K) % N_VALIDATORS)
+        sync = rng.choice(N_VALIDATORS, size=SYNC_K, replace=False).astype(np.uint32)
+        singles = rng.integers(0, N_VALIDATORS, size=2).astype(np.uint32)
+        for a in range(ATT_PER_BLOCK):
+            idx.append(att[a * ATT_K : (a + 1) * ATT_K])
+            pk_off.append(pk_off[-1] + ATT_K)
+        idx.append(sync)
+        pk_off.append(pk_off[-1] + SYNC_K)
+        for s in singles:
+            idx.append(np.array([s], np.uint32))
+            pk_off.append(pk_off[-1] + 1)
+        for k in range(SETS_PER_BLOCK):
+            msgs.append(hashlib.sha256(b"bgv-msg" + seed.to_bytes(8, "little") + (b * SETS_PER_BLOCK + k).to_bytes(4, "little")).digest())
+        n += SETS_PER_BLOCK
+        job_off.append(n)
+    return {
+        "n_sets": n,
+        "n_jobs": len(blocks),
+        "job_offsets": np.array(job_off, np.uint32),
+        "pk_offsets": np.array(pk_off, np.uint32),
+        "pk_indices": np.concatenate(idx).astype(np.uint32),
+        "msgs": np.frombuffer(b"".join(msgs), np.uint8).reshape(n, 32).copy(),
+        "n_raw": 0,
+    }
+
+
+def to_device(arrays: dict, torch, dev):
+    out = dict(arrays)
+    for k, v in arrays.items():
+        if isinstance(v, np.ndarray):
+            t = torch.from_numpy(v.view(np.int32) if v.dtype == np.uint32 else v.view(np.int64) if v.dtype == np.uint64 else v)
+            out[k] = t.to(dev)
+    return out
+
+
+def fpmul_counts():
+    p = os.path.join(ROOT, "profiles", "fpmul_counts.json")
+    return json.load(open(p)) if os.path.exists(p) else None
+
+
+def cpu_baseline(budget_s: float = 15.0):
+    """oracle C restatement (oracle/libbls_ref.so) timed on this host's cores
+    on a bounded sample of the same workload; None when not built."""
+    try:
+        from oracle import cref
+    except Exception as e:  # noqa: BLE001
+        log("cpu_baseline unavailable:", e)
+        return None
+    return cref.bench_segment_sample(budget_s=budget_s, seed=SEED)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--blocks", type=int, default=1024, help="blocks in the segment (1024 = 32 epochs)")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+
+    from lodestar_amd import native
+
+    d = native.Device(local)
+    t0 = time.time()
+    d.gen_keys(0, N_VALIDATORS, SEED)
+    log(f"[bench] {N_VALIDATORS} keys generated in {time.time() - t0:.1f}s")
+
+    my_blocks = [b for b in range(args.blocks) if b % world == rank]
+    arrays = build_segment(my_blocks)
+    darr = to_device(arrays, torch, dev)
+    n_sets = arrays["n_sets"]
+    sigs = torch.zeros((n_sets, 192), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    d.gen_sign(darr, sigs, on_device=True)
+    darr["sigs"] = sigs
+    darr["sig_len"] = torch.full((n_sets,), 96, dtype=torch.int32, device=dev)
+    darr["scalars"] = None  # drawn by the library per call (getrandom)
+    log(f"[bench] rank {rank}: {n_sets} sets signed in {time.time() - t0:.1f}s")
+
+    def step():
+        if world == 1:
+            jr, _ = d.verify(darr, on_device=True, want_set_codes=False)
+            return bool((jr == 1).all())
+        part, _, ok = d.partial(darr, on_device=True)
+        t = torch.frombuffer(bytearray(part), dtype=torch.uint8).to(dev)
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        allp = [p.cpu().numpy().tobytes() for p in parts]
+        return ok and d.combine_final(allp)
+
+    for _ in range(args.warmup):
+        assert step(), "warm-up batch did not verify"
+    stage_sum = np.zeros(native.N_STAGES)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    all_ok = True
+    for _ in range(args.steps):
+        all_ok &= step()
+        stage_sum += np.array(list(d.last_stats.stage_ms))
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        okt = torch.tensor([1 if all_ok else 0], device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        all_ok = bool(okt.item())
+    total_sets = args.blocks * SETS_PER_BLOCK
+    ms_per_step = elapsed / args.steps * 1e3
+    value = total_sets * args.steps / elapsed
+
+    stage_ms = {d.stage_name(i): float(stage_sum[i] / args.steps) for i in range(native.N_STAGES)}
+    # roofline of the dominant kernel (INT32 VALU): algorithmic Fp-mul / launch time
+    roof = None
+    counts = fpmul_counts()
+    if rank == 0:
+        mad_ms = d.bench_mad(256 * 256 * 8, 4096)
+        mad_rate = 256 * 256 * 8 * 4096 * 8 / (mad_ms * 1e-3)  # lane-ops/s
+        peak_fpmul = mad_rate / 288.0 / 1e9
+        fpm_ms = d.bench_fpmul(256 * 256 * 8, 2048)
+        fpm_rate = 256 * 256 * 8 * 2048 / (fpm_ms * 1e-3) / 1e9
+        dom = max(stage_ms, key=stage_ms.get)
+        if counts and dom in counts.get("per_set", {}):
+            per_set = counts["per_set"][dom]
+            shard_sets = arrays["n_sets"]
+            achieved = per_set * shard_sets / (stage_ms[dom] * 1e-3) / 1e9
+            roof = {"bound": "valu-int32", "kernel": dom, "achieved": round(achieved, 3), "peak": round(peak_fpmul, 3),
+                    "unit": "G Fp-mul/s", "frac": round(achieved / peak_fpmul, 4), "traffic": None,
+                    "per_set_fpmul": per_set, "kernel_ms": round(stage_ms[dom], 3),
+                    "mad_u64_lane_ops_per_s": mad_rate, "fpmul_microbench_G_per_s": round(fpm_rate, 3)}
+        else:
+            roof = {"bound": "valu-int32", "kernel": dom, "achieved": None, "peak": round(peak_fpmul, 3),
+                    "unit": "G Fp-mul/s", "frac": None, "traffic": None,
+                    "mad_u64_lane_ops_per_s": mad_rate, "fpmul_microbench_G_per_s": round(fpm_rate, 3)}
+
+    if rank == 0:
+        cpu = None if (args.no_cpu or world > 1) else cpu_baseline()
+        out = {
+            "metric": "BLS signature sets verified/sec (node)",
+            "value": round(value, 1),
+            "unit": "sets/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (device-generated keys/signatures, seeded)",
+            "config": {"workload": "C4 range-sync segment: 32 epochs = %d blocks x 98 sets (95 att k=128, sync k=512, 2 singles), 1M-validator table in HBM" % args.blocks,
+                       "sets": total_sets, "pubkey_refs": int(args.blocks * (ATT_PER_BLOCK * ATT_K + SYNC_K + 2)),
+                       "table_validators": N_VALIDATORS, "jobs": args.blocks, "parallelism": f"shard-by-block x{world}"},
+            "verified": all_ok,
+            "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    d.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -349,25 +349,20 @@ int bgv_verify(bgv_ctx* c, const bgv_batch* b, int32_t* job_result, int32_t* set
 }
 
 // ---- multi-GPU partials ---------------------------------------------------
-static void fp12_to_bytes(uint8_t* out, const fp12_t& f) {
+// fp12 (plain limbs, already out of Montgomery form on the device) <-> 576 B
+static void fp12_plain_to_bytes(uint8_t* out, const fp12_t& f) {
   const fp2_t* cs[6] = {&f.c0.c0, &f.c1.c0, &f.c0.c1, &f.c1.c1, &f.c0.c2, &f.c1.c2};
   for (int k = 0; k < 6; k++) {
-    fp_t t;
-    fp_from_mont(t, cs[k]->c0);
-    fp_to_be48(out + 96 * k, t);
-    fp_from_mont(t, cs[k]->c1);
-    fp_to_be48(out + 96 * k + 48, t);
+    fp_to_be48(out + 96 * k, cs[k]->c0);
+    fp_to_be48(out + 96 * k + 48, cs[k]->c1);
   }
 }
 
-static void fp12_from_bytes(fp12_t& f, const uint8_t* in) {
+static void fp12_plain_from_bytes(fp12_t& f, const uint8_t* in) {
   fp2_t* cs[6] = {&f.c0.c0, &f.c1.c0, &f.c0.c1, &f.c1.c1, &f.c0.c2, &f.c1.c2};
   for (int k = 0; k < 6; k++) {
-    fp_t t;
-    fp_from_be48(t, in + 96 * k);
-    fp_to_mont(cs[k]->c0, t);
-    fp_from_be48(t, in + 96 * k + 48);
-    fp_to_mont(cs[k]->c1, t);
+    fp_from_be48(cs[k]->c0, in + 96 * k);
+    fp_from_be48(cs[k]->c1, in + 96 * k + 48);
   }
 }
 
@@ -381,14 +376,15 @@ int bgv_partial(bgv_ctx* c, const bgv_batch* b, uint8_t* miller576, int32_t* set
   if (int r = work_alloc(c, d.n_sets, d.n_jobs, w)) return r;
   if (int r = run_stages(c, d, w, ST_SIG, ST_BATCH_FINAL)) return r;
   launch_stage(c->st, ST_SET_CODES, d, w);
+  launch_fp12_convert(c->st, w.f_part + 64, w.f_part + 63, 1, false);
   HIPCHK(hipGetLastError());
   fp12_t f;
-  HIPCHK(hipMemcpyAsync(&f, w.f_part + 64, sizeof f, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipMemcpyAsync(&f, w.f_part + 63, sizeof f, hipMemcpyDeviceToHost, c->st));
   std::vector<int32_t> jc(d.n_jobs ? d.n_jobs : 1);
   if (d.n_jobs) HIPCHK(hipMemcpyAsync(jc.data(), w.job_code, (size_t)d.n_jobs * 4, hipMemcpyDeviceToHost, c->st));
   if (set_code && d.n_sets) HIPCHK(hipMemcpyAsync(set_code, w.set_code, (size_t)d.n_sets * 4, hipMemcpyDeviceToHost, c->st));
   HIPCHK(hipStreamSynchronize(c->st));
-  fp12_to_bytes(miller576, f);
+  fp12_plain_to_bytes(miller576, f);
   int32_t ok = 1;
   for (uint32_t j = 0; j < d.n_jobs; j++)
     if (jc[j] != 0) ok = 0;
@@ -400,10 +396,11 @@ int bgv_combine_final(bgv_ctx* c, const uint8_t* parts, uint32_t n, int32_t* is_
   if (!c || (!parts && n) || !is_one) return fail(BGV_E_INVALID_ARG, "null argument");
   HIPCHK(hipSetDevice(c->device));
   std::vector<fp12_t> h(n ? n : 1);
-  for (uint32_t k = 0; k < n; k++) fp12_from_bytes(h[k], parts + 576u * k);
-  if (int r = c->f_part.ensure(n + 65 > 65 ? n + 65 : 65)) return r;
+  for (uint32_t k = 0; k < n; k++) fp12_plain_from_bytes(h[k], parts + 576u * k);
+  if (int r = c->f_part.ensure(2 * (size_t)n + 65)) return r;
   if (int r = c->flags.ensure(4)) return r;
-  if (n) HIPCHK(hipMemcpyAsync(c->f_part.p, h.data(), (size_t)n * sizeof(fp12_t), hipMemcpyHostToDevice, c->st));
+  if (n) HIPCHK(hipMemcpyAsync(c->f_part.p + n, h.data(), (size_t)n * sizeof(fp12_t), hipMemcpyHostToDevice, c->st));
+  launch_fp12_convert(c->st, c->f_part.p + n, c->f_part.p, n, true);
   launch_combine_final(c->st, c->f_part.p, n, c->flags.p);
   HIPCHK(hipGetLastError());
   uint32_t flag = 0;

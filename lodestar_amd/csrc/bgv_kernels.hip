@@ -282,6 +282,21 @@ __global__ void __launch_bounds__(64) k_combine_final(const fp12_t* parts, uint3
   flag[0] = fp12_is_one(r) ? 1u : 0u;
 }
 
+// Montgomery <-> plain limbs for Fp12 values crossing the host boundary
+// (the host never touches the __constant__ curve tables)
+__global__ void __launch_bounds__(64) k_fp12_convert(const fp12_t* in, fp12_t* out, uint32_t n, uint32_t to_mont) {
+  const uint32_t i = gtid();
+  if (i >= n) return;
+  const fp_t* a = (const fp_t*)&in[i];
+  fp_t* r = (fp_t*)&out[i];
+  for (int k = 0; k < 12; k++) {
+    fp_t t = a[k];
+    if (to_mont) fp_to_mont(t, t);
+    else fp_from_mont(t, t);
+    r[k] = t;
+  }
+}
+
 // ======================================================= synthetic data
 // scalar field order r (little-endian u32)
 BGV_CONST uint32_t FR_R[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
@@ -460,6 +475,9 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
 }
 void launch_combine_final(hipStream_t st, const fp12_t* parts, uint32_t n, uint32_t* flag) {
   hipLaunchKernelGGL(k_combine_final, dim3(1), dim3(64), 0, st, parts, n, flag);
+}
+void launch_fp12_convert(hipStream_t st, const fp12_t* in, fp12_t* out, uint32_t n, bool to_mont) {
+  BGV_LAUNCH(k_fp12_convert, n, in, out, n, to_mont ? 1u : 0u);
 }
 void launch_gen_keys(hipStream_t st, g1a* table, uint32_t* sk, uint32_t first, uint32_t n, uint64_t seed) {
   BGV_LAUNCH(k_gen_keys, n, table, sk, first, n, seed);
