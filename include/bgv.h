@@ -114,7 +114,7 @@ typedef struct bgv_batch {
 /* Timings of the last bgv_verify call (ms, HIP events on the context's
  * stream) plus the counters the reference pool exports as
  * lodestar_bls_thread_pool_* metrics (metrics/metrics/lodestar.ts:350-430). */
-#define BGV_N_STAGES 10
+#define BGV_N_STAGES 12
 typedef struct bgv_stats {
   float stage_ms[BGV_N_STAGES]; /* see bgv_stage_name() */
   float total_ms;

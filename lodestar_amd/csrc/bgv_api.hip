@@ -78,7 +78,9 @@ struct bgv_ctx {
   dbuf<int32_t> sig_code, pk_code, job_code, job_result, set_code;
   dbuf<g1a> rpk_aff;
   dbuf<g2j> rsig;
-  dbuf<fp12_t> f_set, f_job, f_part;
+  dbuf<fp12_t> f_set, f_job, f_batch, f_part;
+  dbuf<uint32_t> set_job, s_inf;
+  dbuf<g2a> s_aff;
   // microbench scratch
   dbuf<fp_t> mb_fp;
   dbuf<uint64_t> mb_u64;
@@ -107,9 +109,9 @@ const char* bgv_set_code_name(int code) {
 }
 
 const char* bgv_stage_name(int stage) {
-  static const char* names[ST_COUNT] = {"sig_decode_subgroup", "hash_to_g2", "pk_aggregate_scale", "sig_scale",
-                                        "miller_loop",          "job_reduce", "batch_product",      "batch_final_exp",
-                                        "job_final_exp",        "set_codes"};
+  static const char* names[ST_COUNT] = {"sig_decode_subgroup", "hash_to_g2",    "pk_aggregate_scale", "sig_scale",
+                                        "sig_sum_tree",        "miller_loop",   "miller_product_tree", "batch_product",
+                                        "batch_final_exp",     "job_final_exp", "set_codes"};
   return (stage >= 0 && stage < ST_COUNT) ? names[stage] : "unknown";
 }
 
@@ -140,7 +142,8 @@ int bgv_close(bgv_ctx* c) {
   c->scalars.release(); c->raw_conv.release();
   c->sig_aff.release(); c->h_aff.release(); c->sig_inf.release(); c->flags.release();
   c->sig_code.release(); c->pk_code.release(); c->job_code.release(); c->job_result.release(); c->set_code.release();
-  c->rpk_aff.release(); c->rsig.release(); c->f_set.release(); c->f_job.release(); c->f_part.release();
+  c->rpk_aff.release(); c->rsig.release(); c->f_set.release(); c->f_job.release(); c->f_batch.release(); c->f_part.release();
+  c->set_job.release(); c->s_inf.release(); c->s_aff.release();
   c->mb_fp.release(); c->mb_u64.release();
   (void)hipStreamDestroy(c->st);
   delete c;
@@ -234,11 +237,17 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, std::vector<uin
   d.n_raw = b->n_raw;
   d.table_n = c->table_n;
   d.table = c->table;
+  d.span_log2 = 7;  // device batches: trees cover jobs of <= 128 sets (multithread/index.ts:39)
   if (!b->on_device) {
     // host-side contract checks (the reference rejects these synchronously)
     if (b->job_offsets[0] != 0 || b->job_offsets[J] != n) return fail(BGV_E_INVALID_ARG, "job_offsets must span [0, n_sets]");
-    for (uint32_t j = 0; j < J; j++)
+    uint32_t max_job = 1;
+    for (uint32_t j = 0; j < J; j++) {
       if (b->job_offsets[j + 1] < b->job_offsets[j]) return fail(BGV_E_INVALID_ARG, "job_offsets not monotone");
+      if (b->job_offsets[j + 1] - b->job_offsets[j] > max_job) max_job = b->job_offsets[j + 1] - b->job_offsets[j];
+    }
+    d.span_log2 = 0;
+    while ((1u << d.span_log2) < max_job && d.span_log2 < 16) d.span_log2++;
     if (b->pk_offsets[0] != 0) return fail(BGV_E_INVALID_ARG, "pk_offsets[0] != 0");
     for (uint32_t i = 0; i < n; i++) {
       if (b->pk_offsets[i + 1] < b->pk_offsets[i]) return fail(BGV_E_INVALID_ARG, "pk_offsets not monotone");
@@ -294,14 +303,16 @@ static int work_alloc(bgv_ctx* c, uint32_t n, uint32_t J, dev_work& w) {
   int r = 0;
   if ((r = c->sig_aff.ensure(ns)) || (r = c->h_aff.ensure(ns)) || (r = c->sig_inf.ensure(ns)) ||
       (r = c->sig_code.ensure(ns)) || (r = c->pk_code.ensure(ns)) || (r = c->rpk_aff.ensure(ns)) ||
-      (r = c->rsig.ensure(ns)) || (r = c->f_set.ensure(ns)) || (r = c->set_code.ensure(ns)) ||
-      (r = c->f_job.ensure(nj)) || (r = c->job_code.ensure(nj)) || (r = c->job_result.ensure(nj)) ||
-      (r = c->f_part.ensure(65)) || (r = c->flags.ensure(4)))
+      (r = c->rsig.ensure(ns)) || (r = c->f_set.ensure(ns + nj)) || (r = c->set_code.ensure(ns)) ||
+      (r = c->set_job.ensure(ns)) || (r = c->f_job.ensure(nj)) || (r = c->f_batch.ensure(nj)) ||
+      (r = c->s_aff.ensure(nj)) || (r = c->s_inf.ensure(nj)) || (r = c->job_code.ensure(nj)) ||
+      (r = c->job_result.ensure(nj)) || (r = c->f_part.ensure(4)) || (r = c->flags.ensure(4)))
     return r;
   w.sig_aff = c->sig_aff.p; w.h_aff = c->h_aff.p; w.sig_inf = c->sig_inf.p; w.sig_code = c->sig_code.p;
   w.pk_code = c->pk_code.p; w.rpk_aff = c->rpk_aff.p; w.rsig = c->rsig.p; w.f_set = c->f_set.p;
   w.set_code = c->set_code.p; w.f_job = c->f_job.p; w.job_code = c->job_code.p; w.job_result = c->job_result.p;
   w.f_part = c->f_part.p; w.flags = c->flags.p;
+  w.set_job = c->set_job.p; w.f_batch = c->f_batch.p; w.s_aff = c->s_aff.p; w.s_inf = c->s_inf.p;
   return 0;
 }
 
@@ -376,10 +387,15 @@ int bgv_partial(bgv_ctx* c, const bgv_batch* b, uint8_t* miller576, int32_t* set
   if (int r = work_alloc(c, d.n_sets, d.n_jobs, w)) return r;
   if (int r = run_stages(c, d, w, ST_SIG, ST_BATCH_FINAL)) return r;
   launch_stage(c->st, ST_SET_CODES, d, w);
-  launch_fp12_convert(c->st, w.f_part + 64, w.f_part + 63, 1, false);
-  HIPCHK(hipGetLastError());
   fp12_t f;
-  HIPCHK(hipMemcpyAsync(&f, w.f_part + 63, sizeof f, hipMemcpyDeviceToHost, c->st));
+  if (d.n_jobs) {
+    launch_fp12_convert(c->st, w.f_batch, w.f_part, 1, false);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(&f, w.f_part, sizeof f, hipMemcpyDeviceToHost, c->st));
+  } else {
+    memset(&f, 0, sizeof f);
+    f.c0.c0.c0.l[0] = 1;  // plain 1
+  }
   std::vector<int32_t> jc(d.n_jobs ? d.n_jobs : 1);
   if (d.n_jobs) HIPCHK(hipMemcpyAsync(jc.data(), w.job_code, (size_t)d.n_jobs * 4, hipMemcpyDeviceToHost, c->st));
   if (set_code && d.n_sets) HIPCHK(hipMemcpyAsync(set_code, w.set_code, (size_t)d.n_sets * 4, hipMemcpyDeviceToHost, c->st));

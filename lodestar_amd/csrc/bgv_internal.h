@@ -15,6 +15,7 @@ enum : int32_t {
 // indexed by set (or job); see include/bgv.h bgv_batch for their meaning.
 struct dev_batch {
   uint32_t n_sets, n_jobs, n_raw, table_n;
+  uint32_t span_log2;  // per-job reduction tree covers 2^span_log2 sets
   const uint32_t* job_off;
   const uint32_t* pk_off;
   const uint32_t* pk_idx;
@@ -35,12 +36,16 @@ struct dev_work {
   g1a* rpk_aff;       // [r_i] aggregated pubkey, affine
   int32_t* pk_code;
   g2j* rsig;          // [r_i] sigma_i
-  fp12_t* f_set;      // per-set Miller value
+  uint32_t* set_job;  // job id of every set
+  g2a* s_aff;         // per job: sum [r_i] sigma_i, affine
+  uint32_t* s_inf;
+  fp12_t* f_set;      // per pair Miller value: n_sets set pairs, then n_jobs (-G1, S_job) pairs
   fp12_t* f_job;      // per-job Miller product (incl. the -G1 pair)
+  fp12_t* f_batch;    // batch product tree scratch [n_jobs]
   int32_t* job_code;
   int32_t* job_result;
   int32_t* set_code;
-  fp12_t* f_part;     // [65] batch product scratch; [64] = whole batch
+  fp12_t* f_part;     // conversion scratch for partials
   uint32_t* flags;    // [0] = whole batch verified
 };
 
@@ -49,8 +54,9 @@ enum Stage {
   ST_HASH,
   ST_PK,
   ST_SIG_SCALE,
+  ST_S_TREE,
   ST_MILLER,
-  ST_JOB,
+  ST_F_TREE,
   ST_BATCH_PROD,
   ST_BATCH_FINAL,
   ST_JOB_FINAL,

@@ -24,6 +24,13 @@
 
 namespace bgv {
 
+// Occupancy of the per-set kernels: minimum waves per SIMD requested from the
+// register allocator (1 = up to 512 VGPR+AGPR per lane).  Tuned on MI355X.
+#ifndef BGV_WAVES
+#define BGV_WAVES 2
+#endif
+#define BGV_BULK __launch_bounds__(64, BGV_WAVES)
+
 __device__ __forceinline__ uint32_t gtid() { return blockIdx.x * blockDim.x + threadIdx.x; }
 
 // ---------------------------------------------------------------- helpers
@@ -43,7 +50,7 @@ __device__ __forceinline__ void load_pk(g1a& out, const dev_batch& b, uint32_t i
 // ------------------------------------------------------------ k_raw_pks
 // uncompressed 96 B big-endian, trusted (multithread/worker.ts:108-114:
 // PublicKey.fromBytes(.., affine) without validation); infinity -> (0, 0)
-__global__ void __launch_bounds__(64) k_raw_pks(const uint8_t* raw, g1a* out, uint32_t n) {
+__global__ void BGV_BULK k_raw_pks(const uint8_t* raw, g1a* out, uint32_t n) {
   const uint32_t i = gtid();
   if (i >= n) return;
   g1a p;
@@ -52,7 +59,7 @@ __global__ void __launch_bounds__(64) k_raw_pks(const uint8_t* raw, g1a* out, ui
 }
 
 // compressed 48 B table load (syncPubkeys path); bad keys -> (0, 0)
-__global__ void __launch_bounds__(64) k_table_from_compressed(const uint8_t* in48, g1a* out, uint32_t n) {
+__global__ void BGV_BULK k_table_from_compressed(const uint8_t* in48, g1a* out, uint32_t n) {
   const uint32_t i = gtid();
   if (i >= n) return;
   g1a p;
@@ -61,7 +68,7 @@ __global__ void __launch_bounds__(64) k_table_from_compressed(const uint8_t* in4
   out[i] = p;
 }
 
-__global__ void __launch_bounds__(64) k_table_from_uncompressed(const uint8_t* in96, g1a* out, uint32_t n) {
+__global__ void BGV_BULK k_table_from_uncompressed(const uint8_t* in96, g1a* out, uint32_t n) {
   const uint32_t i = gtid();
   if (i >= n) return;
   g1a p;
@@ -69,7 +76,7 @@ __global__ void __launch_bounds__(64) k_table_from_uncompressed(const uint8_t* i
   out[i] = p;
 }
 
-__global__ void __launch_bounds__(64) k_table_export(const g1a* tab, uint8_t* out96, uint32_t n) {
+__global__ void BGV_BULK k_table_export(const g1a* tab, uint8_t* out96, uint32_t n) {
   const uint32_t i = gtid();
   if (i >= n) return;
   const g1a p = tab[i];
@@ -87,7 +94,7 @@ __global__ void __launch_bounds__(64) k_table_export(const g1a* tab, uint8_t* ou
 }
 
 // ------------------------------------------------------------------ k_sig
-__global__ void __launch_bounds__(64) k_sig(dev_batch b, dev_work w) {
+__global__ void BGV_BULK k_sig(dev_batch b, dev_work w) {
   const uint32_t i = gtid();
   if (i >= b.n_sets) return;
   const uint32_t len = b.sig_len[i];
@@ -110,7 +117,7 @@ __global__ void __launch_bounds__(64) k_sig(dev_batch b, dev_work w) {
 }
 
 // ----------------------------------------------------------------- k_hash
-__global__ void __launch_bounds__(64) k_hash(dev_batch b, dev_work w) {
+__global__ void BGV_BULK k_hash(dev_batch b, dev_work w) {
   const uint32_t i = gtid();
   if (i >= b.n_sets) return;
   uint8_t m[32];
@@ -124,7 +131,7 @@ __global__ void __launch_bounds__(64) k_hash(dev_batch b, dev_work w) {
 }
 
 // ------------------------------------------------------------------- k_pk
-__global__ void __launch_bounds__(64) k_pk(dev_batch b, dev_work w) {
+__global__ void BGV_BULK k_pk(dev_batch b, dev_work w) {
   const uint32_t i = gtid();
   if (i >= b.n_sets) return;
   const uint32_t beg = b.pk_off[i], end = b.pk_off[i + 1];
@@ -153,7 +160,7 @@ __global__ void __launch_bounds__(64) k_pk(dev_batch b, dev_work w) {
 }
 
 // ------------------------------------------------------------ k_sig_scale
-__global__ void __launch_bounds__(64) k_sig_scale(dev_batch b, dev_work w) {
+__global__ void BGV_BULK k_sig_scale(dev_batch b, dev_work w) {
   const uint32_t i = gtid();
   if (i >= b.n_sets) return;
   g2j r;
@@ -167,21 +174,32 @@ __global__ void __launch_bounds__(64) k_sig_scale(dev_batch b, dev_work w) {
   w.rsig[i] = r;
 }
 
-// --------------------------------------------------------------- k_miller
-__global__ void __launch_bounds__(64) k_miller(dev_batch b, dev_work w) {
-  const uint32_t i = gtid();
-  if (i >= b.n_sets) return;
-  fp12_t f;
-  if (w.sig_code[i] != C_OK || w.pk_code[i] != C_OK) {
-    fp12_one(f);
-  } else {
-    miller_loop(f, w.rpk_aff[i], false, w.h_aff[i], false);
-  }
-  w.f_set[i] = f;
+// ------------------------------------------------------ per-job S tree
+// Sum of [r_i] sigma_i per job as a segmented pairwise tree: level `s`
+// folds element i + s into i for every i at an even multiple of s inside
+// its job.  log2(job size) launches replace a serial per-job loop (the
+// first levels run on n/2 lanes, so the latency cost is one G2 add per level).
+__global__ void BGV_BULK k_set_job(dev_batch b, dev_work w) {
+  const uint32_t j = gtid();
+  if (j >= b.n_jobs) return;
+  for (uint32_t i = b.job_off[j]; i < b.job_off[j + 1]; i++) w.set_job[i] = j;
 }
 
-// ------------------------------------------------------------------ k_job
-__global__ void __launch_bounds__(64) k_job(dev_batch b, dev_work w) {
+__global__ void BGV_BULK k_s_level(dev_batch b, dev_work w, uint32_t s) {
+  const uint32_t i = gtid();
+  if (i >= b.n_sets) return;
+  const uint32_t j = w.set_job[i];
+  const uint32_t beg = b.job_off[j], end = b.job_off[j + 1];
+  if (((i - beg) % (2 * s)) != 0 || i + s >= end) return;
+  g2j a = w.rsig[i];
+  const g2j c = w.rsig[i + s];
+  jac_add(a, a, c);
+  w.rsig[i] = a;
+}
+
+// per job: first parse error (set order), S_job -> affine as the job's
+// extra Miller pair (-G1, S_job) at pair index n_sets + j
+__global__ void BGV_BULK k_job_s(dev_batch b, dev_work w, uint32_t span) {
   const uint32_t j = gtid();
   if (j >= b.n_jobs) return;
   const uint32_t beg = b.job_off[j], end = b.job_off[j + 1];
@@ -191,62 +209,94 @@ __global__ void __launch_bounds__(64) k_job(dev_batch b, dev_work w) {
   for (uint32_t i = beg; i < end && code == C_OK; i++) code = w.sig_code[i];
   for (uint32_t i = beg; i < end && code == C_OK; i++) code = w.pk_code[i];
   if (end == beg) code = C_EMPTY_JOB;
-  fp12_t f;
-  fp12_one(f);
+  g2a sa;
+  sa.x = fp2_zero();
+  sa.y = fp2_zero();
+  uint32_t inf = 1;
   if (code == C_OK) {
-    g2j s;
-    jac_set_inf(s);
-    bool first = true;
-    for (uint32_t i = beg; i < end; i++) {
+    g2j s = w.rsig[beg];
+    for (uint32_t i = beg + span; i < end; i += span) {  // jobs larger than the tree
       const g2j r = w.rsig[i];
       jac_add(s, s, r);
-      if (first) { f = w.f_set[i]; first = false; }
-      else fp12_mul(f, f, w.f_set[i]);
     }
-    g2a sa;
-    if (jac_to_aff(sa, s)) {
-      g1a ng;
-      ng.x = G1_X_MONT;
-      ng.y = G1_NEG_Y_MONT;
-      fp12_t g;
-      miller_loop(g, ng, false, sa, false);
-      fp12_mul(f, f, g);
-    }
+    inf = jac_to_aff(sa, s) ? 0u : 1u;
   }
-  w.f_job[j] = f;
+  w.s_aff[j] = sa;
+  w.s_inf[j] = inf;
   w.job_code[j] = code;
 }
 
-// ---------------------------------------------------------- k_batch_final
-// One workgroup of 64 lanes: lane l multiplies jobs l, l+64, ...; lane 0
-// folds the 64 partials and runs the single final exponentiation.
-__global__ void __launch_bounds__(64) k_batch_prod(dev_batch b, dev_work w) {
-  const uint32_t l = threadIdx.x;
+// --------------------------------------------------------------- k_miller
+// One launch over n_sets + n_jobs pairs: (r_i PK_i, H(m_i)) for every set,
+// then (-G1, S_job) for every job.
+__global__ void BGV_BULK k_miller(dev_batch b, dev_work w) {
+  const uint32_t t = gtid();
+  if (t >= b.n_sets + b.n_jobs) return;
   fp12_t f;
-  fp12_one(f);
-  bool any = false;
-  for (uint32_t j = l; j < b.n_jobs; j += 64) {
-    if (w.job_code[j] != C_OK) continue;
-    if (!any) { f = w.f_job[j]; any = true; }
-    else fp12_mul(f, f, w.f_job[j]);
+  if (t < b.n_sets) {
+    if (w.sig_code[t] != C_OK || w.pk_code[t] != C_OK) fp12_one(f);
+    else miller_loop(f, w.rpk_aff[t], false, w.h_aff[t], false);
+  } else {
+    const uint32_t j = t - b.n_sets;
+    g1a ng;
+    ng.x = G1_X_MONT;
+    ng.y = G1_NEG_Y_MONT;
+    if (w.job_code[j] != C_OK || w.s_inf[j]) fp12_one(f);
+    else miller_loop(f, ng, false, w.s_aff[j], false);
   }
-  w.f_part[l] = f;
-  __syncthreads();
-  if (l != 0) return;
-  fp12_t g = w.f_part[0];
-  for (int k = 1; k < 64; k++) fp12_mul(g, g, w.f_part[k]);
-  w.f_part[64] = g;
+  w.f_set[t] = f;
 }
 
-__global__ void __launch_bounds__(64) k_batch_final(dev_batch b, dev_work w) {
+// ------------------------------------------------------ per-job f tree
+__global__ void BGV_BULK k_f_level(dev_batch b, dev_work w, uint32_t s) {
+  const uint32_t i = gtid();
+  if (i >= b.n_sets) return;
+  const uint32_t j = w.set_job[i];
+  const uint32_t beg = b.job_off[j], end = b.job_off[j + 1];
+  if (((i - beg) % (2 * s)) != 0 || i + s >= end) return;
+  fp12_t a = w.f_set[i];
+  fp12_mul(a, a, w.f_set[i + s]);
+  w.f_set[i] = a;
+}
+
+__global__ void BGV_BULK k_job_f(dev_batch b, dev_work w, uint32_t span) {
+  const uint32_t j = gtid();
+  if (j >= b.n_jobs) return;
+  const uint32_t beg = b.job_off[j], end = b.job_off[j + 1];
+  fp12_t f;
+  if (w.job_code[j] != C_OK) {
+    fp12_one(f);  // rejected jobs take no part in the batch product
+  } else {
+    f = w.f_set[beg];
+    for (uint32_t i = beg + span; i < end; i += span) fp12_mul(f, f, w.f_set[i]);
+    fp12_mul(f, f, w.f_set[b.n_sets + j]);
+  }
+  w.f_job[j] = f;
+  w.f_batch[j] = f;
+}
+
+// ---------------------------------------------------------- batch product
+__global__ void BGV_BULK k_batch_level(dev_batch b, dev_work w, uint32_t s) {
+  const uint32_t j = gtid();
+  if (j >= b.n_jobs || (j % (2 * s)) != 0 || j + s >= b.n_jobs) return;
+  fp12_t a = w.f_batch[j];
+  fp12_mul(a, a, w.f_batch[j + s]);
+  w.f_batch[j] = a;
+}
+
+__global__ void BGV_BULK k_batch_final(dev_batch b, dev_work w) {
   if (threadIdx.x != 0) return;
+  if (b.n_jobs == 0) {
+    w.flags[0] = 0u;
+    return;
+  }
   fp12_t r;
-  fp12_final_exp(r, w.f_part[64]);
+  fp12_final_exp(r, w.f_batch[0]);
   w.flags[0] = fp12_is_one(r) ? 1u : 0u;
 }
 
 // ------------------------------------------------------------ k_job_final
-__global__ void __launch_bounds__(64) k_job_final(dev_batch b, dev_work w) {
+__global__ void BGV_BULK k_job_final(dev_batch b, dev_work w) {
   const uint32_t j = gtid();
   if (j >= b.n_jobs) return;
   const int32_t code = w.job_code[j];
@@ -264,7 +314,7 @@ __global__ void __launch_bounds__(64) k_job_final(dev_batch b, dev_work w) {
 }
 
 // set codes for the host: signature code first, then the pubkey code
-__global__ void __launch_bounds__(64) k_set_codes(dev_batch b, dev_work w) {
+__global__ void BGV_BULK k_set_codes(dev_batch b, dev_work w) {
   const uint32_t i = gtid();
   if (i >= b.n_sets) return;
   const int32_t c = w.sig_code[i];
@@ -272,7 +322,7 @@ __global__ void __launch_bounds__(64) k_set_codes(dev_batch b, dev_work w) {
 }
 
 // ------------------------------------------------- multi-GPU combination
-__global__ void __launch_bounds__(64) k_combine_final(const fp12_t* parts, uint32_t n, uint32_t* flag) {
+__global__ void BGV_BULK k_combine_final(const fp12_t* parts, uint32_t n, uint32_t* flag) {
   if (threadIdx.x != 0) return;
   fp12_t g;
   fp12_one(g);
@@ -284,7 +334,7 @@ __global__ void __launch_bounds__(64) k_combine_final(const fp12_t* parts, uint3
 
 // Montgomery <-> plain limbs for Fp12 values crossing the host boundary
 // (the host never touches the __constant__ curve tables)
-__global__ void __launch_bounds__(64) k_fp12_convert(const fp12_t* in, fp12_t* out, uint32_t n, uint32_t to_mont) {
+__global__ void BGV_BULK k_fp12_convert(const fp12_t* in, fp12_t* out, uint32_t n, uint32_t to_mont) {
   const uint32_t i = gtid();
   if (i >= n) return;
   const fp_t* a = (const fp_t*)&in[i];
@@ -363,7 +413,7 @@ __device__ void gen_sk(uint32_t sk[8], uint64_t seed, uint32_t i) {
   while (u256_ge_r(sk)) u256_sub_r(sk);
 }
 
-__global__ void __launch_bounds__(64) k_gen_keys(g1a* table, uint32_t* sk_store, uint32_t first, uint32_t n,
+__global__ void BGV_BULK k_gen_keys(g1a* table, uint32_t* sk_store, uint32_t first, uint32_t n,
                                                  uint64_t seed) {
   const uint32_t t = gtid();
   if (t >= n) return;
@@ -396,7 +446,7 @@ BGV_NI void g2_compress(uint8_t* out, const g2j& p) {
   for (int k = 0; k < 96; k++) out[k] = buf[k];
 }
 
-__global__ void __launch_bounds__(64) k_gen_sign(dev_batch b, const uint32_t* sk_store, uint8_t* sigs_out) {
+__global__ void BGV_BULK k_gen_sign(dev_batch b, const uint32_t* sk_store, uint8_t* sigs_out) {
   const uint32_t i = gtid();
   if (i >= b.n_sets) return;
   uint32_t s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -459,20 +509,32 @@ void launch_table_export(hipStream_t st, const g1a* tab, uint8_t* out, uint32_t 
   BGV_LAUNCH(k_table_export, n, tab, out, n);
 }
 void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work& w) {
+  const uint32_t span = 1u << b.span_log2;
   switch (stage) {
     case ST_SIG: BGV_LAUNCH(k_sig, b.n_sets, b, w); break;
     case ST_HASH: BGV_LAUNCH(k_hash, b.n_sets, b, w); break;
     case ST_PK: BGV_LAUNCH(k_pk, b.n_sets, b, w); break;
     case ST_SIG_SCALE: BGV_LAUNCH(k_sig_scale, b.n_sets, b, w); break;
-    case ST_MILLER: BGV_LAUNCH(k_miller, b.n_sets, b, w); break;
-    case ST_JOB: BGV_LAUNCH(k_job, b.n_jobs, b, w); break;
-    case ST_BATCH_PROD: hipLaunchKernelGGL(k_batch_prod, dim3(1), dim3(64), 0, st, b, w); break;
+    case ST_S_TREE:
+      BGV_LAUNCH(k_set_job, b.n_jobs, b, w);
+      for (uint32_t s = 1; s < span; s *= 2) BGV_LAUNCH(k_s_level, b.n_sets, b, w, s);
+      BGV_LAUNCH(k_job_s, b.n_jobs, b, w, span);
+      break;
+    case ST_MILLER: BGV_LAUNCH(k_miller, b.n_sets + b.n_jobs, b, w); break;
+    case ST_F_TREE:
+      for (uint32_t s = 1; s < span; s *= 2) BGV_LAUNCH(k_f_level, b.n_sets, b, w, s);
+      BGV_LAUNCH(k_job_f, b.n_jobs, b, w, span);
+      break;
+    case ST_BATCH_PROD:
+      for (uint32_t s = 1; s < b.n_jobs; s *= 2) BGV_LAUNCH(k_batch_level, b.n_jobs, b, w, s);
+      break;
     case ST_BATCH_FINAL: hipLaunchKernelGGL(k_batch_final, dim3(1), dim3(64), 0, st, b, w); break;
     case ST_JOB_FINAL: BGV_LAUNCH(k_job_final, b.n_jobs, b, w); break;
     case ST_SET_CODES: BGV_LAUNCH(k_set_codes, b.n_sets, b, w); break;
     default: break;
   }
 }
+
 void launch_combine_final(hipStream_t st, const fp12_t* parts, uint32_t n, uint32_t* flag) {
   hipLaunchKernelGGL(k_combine_final, dim3(1), dim3(64), 0, st, parts, n, flag);
 }

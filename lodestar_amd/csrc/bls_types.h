@@ -10,11 +10,20 @@
 #define BGV_HDN __host__ __device__ __noinline__
 #define BGV_CONST __constant__ const
 #define BGV_NI static __host__ __device__ __noinline__
+#ifndef BGV_FP2_INLINE
+#define BGV_FP2_INLINE 0
+#endif
+#if BGV_FP2_INLINE
+#define BGV_NI2 BGV_HD
+#else
+#define BGV_NI2 BGV_NI
+#endif
 #else
 #define BGV_HD static inline
 #define BGV_HDN static
 #define BGV_CONST static const
 #define BGV_NI static inline
+#define BGV_NI2 static inline
 #endif
 
 namespace bgv {

@@ -103,7 +103,13 @@ BGV_HD void fp_neg(fp_t& r, const fp_t& a) {
 // Montgomery product r = a * b / R mod p.
 // Operand-scanning CIOS with the "spare top bit" shortcut: p's top limb is
 // < 2^29, so the running sum never needs a 13th/14th word (t < 2p throughout).
+#ifdef BGV_COUNT_OPS
+extern unsigned long long bgv_fpmul_count;  // host op-count build only (tools/opcount.cpp)
+#endif
 BGV_HD void fp_mul(fp_t& r, const fp_t& a, const fp_t& b) {
+#ifdef BGV_COUNT_OPS
+  bgv_fpmul_count++;
+#endif
   uint32_t t[NL];
 #pragma unroll
   for (int i = 0; i < NL; i++) t[i] = 0;

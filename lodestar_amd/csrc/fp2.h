@@ -26,7 +26,7 @@ BGV_HD void fp2_mul4(fp2_t& r, const fp2_t& a) { fp_mul4(r.c0, a.c0); fp_mul4(r.
 BGV_HD void fp2_mul8(fp2_t& r, const fp2_t& a) { fp_mul8(r.c0, a.c0); fp_mul8(r.c1, a.c1); }
 
 // Karatsuba: 3 Fp products
-BGV_NI void fp2_mul(fp2_t& r, const fp2_t& a, const fp2_t& b) {
+BGV_NI2 void fp2_mul(fp2_t& r, const fp2_t& a, const fp2_t& b) {
   fp_t t0, t1, t2, t3;
   fp_mul(t0, a.c0, b.c0);
   fp_mul(t1, a.c1, b.c1);
@@ -39,7 +39,7 @@ BGV_NI void fp2_mul(fp2_t& r, const fp2_t& a, const fp2_t& b) {
 }
 
 // complex squaring: 2 Fp products
-BGV_NI void fp2_sqr(fp2_t& r, const fp2_t& a) {
+BGV_NI2 void fp2_sqr(fp2_t& r, const fp2_t& a) {
   fp_t t0, t1, t2;
   fp_add(t0, a.c0, a.c1);
   fp_sub(t1, a.c0, a.c1);
@@ -48,7 +48,7 @@ BGV_NI void fp2_sqr(fp2_t& r, const fp2_t& a) {
   fp_dbl(r.c1, t2);
 }
 
-BGV_NI void fp2_mul_fp(fp2_t& r, const fp2_t& a, const fp_t& b) { fp_mul(r.c0, a.c0, b); fp_mul(r.c1, a.c1, b); }
+BGV_NI2 void fp2_mul_fp(fp2_t& r, const fp2_t& a, const fp_t& b) { fp_mul(r.c0, a.c0, b); fp_mul(r.c1, a.c1, b); }
 
 // multiply by the tower non-residue xi = 1 + i
 BGV_HD void fp2_mul_xi(fp2_t& r, const fp2_t& a) {

@@ -14,7 +14,7 @@ import threading
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libbgv.so")
+LIB_PATH = os.environ.get("BGV_LIB", os.path.join(HERE, "libbgv.so"))
 
 # include/bgv.h enums
 BGV_OK = 0
@@ -40,7 +40,7 @@ SET_CODE_NAMES = {
 
 PK_COMPRESSED_48 = 0
 PK_UNCOMPRESSED_96 = 1
-N_STAGES = 10
+N_STAGES = 12
 
 EXPORTS = [
     "bgv_abi_version", "bgv_set_code_name", "bgv_stage_name", "bgv_last_error", "bgv_open", "bgv_close",

@@ -27,15 +27,15 @@ def stale(lib=LIB):
     return any(os.path.getmtime(d) > t for d in deps())
 
 
-def build(force=False, verbose=False):
-    if not force and not stale():
-        return LIB
+def build(force=False, verbose=False, lib=LIB, defines=()):
+    if not force and not stale(lib):
+        return lib
     objs = []
     procs = []
     for s in SOURCES:
-        o = os.path.join(CSRC, s.replace(".hip", ".o"))
+        o = os.path.join(CSRC, os.path.basename(lib) + "." + s.replace(".hip", ".o"))
         cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-               "-I" + os.path.join(ROOT, "include"), "-c", os.path.join(CSRC, s), "-o", o]
+               "-I" + os.path.join(ROOT, "include")] + ["-D" + x for x in defines] + ["-c", os.path.join(CSRC, s), "-o", o]
         if verbose:
             print(" ".join(cmd), flush=True)
         procs.append(subprocess.Popen(cmd))
@@ -43,14 +43,18 @@ def build(force=False, verbose=False):
     for p in procs:
         if p.wait() != 0:
             raise RuntimeError("hipcc failed")
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs)
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     for o in objs:
         os.remove(o)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, verbose=True)
-    print(LIB)
+    if "--variants" in sys.argv:  # occupancy experiment builds
+        for w in (1, 2, 4):
+            print(build(force=True, lib=LIB.replace(".so", f"_w{w}.so"), defines=[f"BGV_WAVES={w}"]))
+    else:
+        build(force="--force" in sys.argv, verbose=True)
+        print(LIB)

@@ -1,0 +1,87 @@
+// Instrumented HOST build of the device arithmetic (lodestar_amd/csrc/*.h)
+// that counts Montgomery Fp products per pipeline stage -- the algorithmic
+// work W used for the roofline ("frozen by the instrumented
+// restatement").  Same code, same formulas as the kernels in
+// bgv_kernels.hip, stage by stage.  Prints JSON.
+#define BGV_COUNT_OPS 1
+#include <stdio.h>
+#include <stdlib.h>
+#include "../lodestar_amd/csrc/pairing.h"
+namespace bgv { unsigned long long bgv_fpmul_count = 0; }
+using namespace bgv;
+
+static uint64_t rng = 0x243f6a8885a308d3ull;
+static uint64_t rnd64() { rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17; return rng; }
+
+int main(int argc, char** argv) {
+  const int k_att = 128, k_sync = 512, per_block = 98;
+  // inputs: a valid signature = H(m') compressed, H(m) of a message, table points = multiples of G1
+  uint8_t m[32], m2[32];
+  for (int i = 0; i < 32; i++) { m[i] = (uint8_t)(i * 7 + 1); m2[i] = (uint8_t)(i * 3 + 5); }
+  g2j hs; hash_to_g2(hs, m2);
+  g2a hsa; jac_to_aff(hsa, hs);
+  uint8_t sig[96];
+  { fp_t t; fp_from_mont(t, hsa.x.c1); fp_to_be48(sig, t); fp_from_mont(t, hsa.x.c0); fp_to_be48(sig + 48, t);
+    sig[0] |= 0x80 | (fp2_lex_largest(hsa.y) ? 0x20 : 0); }
+  g1a pts[64];
+  { g1j g, acc; g.x = G1_X_MONT; g.y = G1_Y_MONT; fe_one(g.z); acc = g;
+    for (int i = 0; i < 64; i++) { jac_dbl(acc, acc); jac_add(acc, acc, g); jac_to_aff(pts[i], acc); } }
+
+  const int reps = 64;
+  double sig_c = 0, hash_c = 0, pk_add_c = 0, pk_fix_c = 0, sig_scale_c = 0, miller_c = 0, fmul_c = 0, g2add_c = 0, aff2_c = 0, fe_c = 0;
+  for (int r = 0; r < reps; r++) {
+    uint64_t sc = rnd64() | (1ull << 63);  // full 64-bit random scalar (top bit set: worst case)
+    sc = rnd64(); if (!sc) sc = 1;
+    bgv_fpmul_count = 0;
+    g2a a; bool inf; g2_decompress(a, inf, sig); g2j j; jac_from_aff(j, a); (void)g2_in_subgroup(j);
+    sig_c += bgv_fpmul_count;
+    bgv_fpmul_count = 0;
+    g2j h; hash_to_g2(h, m); g2a ha; jac_to_aff(ha, h);
+    hash_c += bgv_fpmul_count;
+    // pk: one mixed add per additional pubkey
+    g1j acc; jac_from_aff(acc, pts[0]);
+    bgv_fpmul_count = 0;
+    for (int i = 1; i < 64; i++) jac_add_aff(acc, acc, pts[i]);
+    pk_add_c += (double)bgv_fpmul_count / 63.0;
+    bgv_fpmul_count = 0;
+    g1j rp; jac_mul_u64(rp, acc, sc); g1a rpa; jac_to_aff(rpa, rp);
+    pk_fix_c += bgv_fpmul_count;
+    bgv_fpmul_count = 0;
+    g2j s2; jac_from_aff(s2, a); g2j rs; jac_mul_u64(rs, s2, sc);
+    sig_scale_c += bgv_fpmul_count;
+    bgv_fpmul_count = 0;
+    g2j t2 = rs; jac_add(t2, t2, rs); jac_add(t2, t2, s2);
+    g2add_c += bgv_fpmul_count / 2.0;
+    bgv_fpmul_count = 0;
+    g2a t2a; jac_to_aff(t2a, t2);
+    aff2_c += bgv_fpmul_count;
+    bgv_fpmul_count = 0;
+    fp12_t f; miller_loop(f, rpa, false, ha, false);
+    miller_c += bgv_fpmul_count;
+    bgv_fpmul_count = 0;
+    fp12_t g; fp12_mul(g, f, f);
+    fmul_c += bgv_fpmul_count;
+    if (r == 0) { bgv_fpmul_count = 0; fp12_t e; fp12_final_exp(e, f); fe_c = bgv_fpmul_count; }
+  }
+  sig_c /= reps; hash_c /= reps; pk_add_c /= reps; pk_fix_c /= reps; sig_scale_c /= reps; miller_c /= reps;
+  fmul_c /= reps; g2add_c /= reps; aff2_c /= reps;
+  // C4 block mix: 95 sets of k=128, 1 of k=512, 2 singles -> mean pubkeys per set
+  const double mean_k = (95.0 * k_att + k_sync + 2.0) / per_block;
+  const double pk_c = (mean_k - 1.0) * pk_add_c + pk_fix_c;
+  // trees per set (C4: 98 sets per job, 1024 jobs)
+  const double s_tree = g2add_c * (per_block - 1.0) / per_block + aff2_c / per_block;
+  const double f_tree = fmul_c * (per_block) / per_block;  // (98-1) set products + the job pair, per set
+  printf("{\n \"generator\": \"tools/opcount.cpp (instrumented host build of lodestar_amd/csrc)\",\n");
+  printf(" \"unit\": \"Montgomery Fp products (fp_mul calls, squares included) per signature set\",\n");
+  printf(" \"workload\": \"C4 block mix: 95 x k=128, 1 x k=512, 2 x k=1 per 98-set job; random 64-bit scalars\",\n");
+  printf(" \"mean_pubkeys_per_set\": %.3f,\n", mean_k);
+  printf(" \"components\": {\"g2_decompress_subgroup\": %.1f, \"hash_to_g2_affine\": %.1f, \"g1_mixed_add\": %.2f, "
+         "\"g1_mul_u64_affine\": %.1f, \"g2_mul_u64\": %.1f, \"g2_add\": %.1f, \"g2_to_affine\": %.1f, \"miller_loop_pair\": %.1f, "
+         "\"fp12_mul\": %.1f, \"final_exp\": %.1f},\n",
+         sig_c, hash_c, pk_add_c, pk_fix_c, sig_scale_c, g2add_c, aff2_c, miller_c, fmul_c, fe_c);
+  printf(" \"per_set\": {\"sig_decode_subgroup\": %.1f, \"hash_to_g2\": %.1f, \"pk_aggregate_scale\": %.1f, \"sig_scale\": %.1f, "
+         "\"sig_sum_tree\": %.1f, \"miller_loop\": %.1f, \"miller_product_tree\": %.1f},\n",
+         sig_c, hash_c, pk_c, sig_scale_c, s_tree, miller_c * (1.0 + 1.0 / per_block), f_tree);
+  printf(" \"per_set_total\": %.1f\n}\n", sig_c + hash_c + pk_c + sig_scale_c + s_tree + miller_c * (1.0 + 1.0 / per_block) + f_tree);
+  return 0;
+}
