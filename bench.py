@@ -101,7 +101,7 @@ def fpmul_counts():
     return json.load(open(p)) if os.path.exists(p) else None
 
 
-def cpu_baseline(budget_s: float = 15.0):
+def cpu_baseline(budget_s: float = 10.0):
     """oracle C restatement (oracle/libbls_ref.so) timed on this host's cores
     on a bounded sample of the same workload; None when not built."""
     try:
