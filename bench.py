@@ -119,6 +119,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--blocks", type=int, default=1024, help="blocks in the segment (1024 = 32 epochs)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-c2", action="store_true", help="skip the C2 latency leg (profiling runs)")
     args = ap.parse_args()
 
     import torch
@@ -194,7 +195,7 @@ def main():
 
     # C2 gossip batch latency: 64 sets x 128 pubkeys, one job, host -> device -> verdict
     c2 = None
-    if rank == 0:
+    if rank == 0 and not args.no_c2:
         g = build_segment([0], seed=SEED + 1000)
         n2, k2 = 64, ATT_K
         c2a = {"n_sets": n2, "n_jobs": 1, "job_offsets": np.array([0, n2], np.uint32),

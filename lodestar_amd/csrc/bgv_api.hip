@@ -77,6 +77,8 @@ struct bgv_ctx {
   dbuf<uint32_t> sig_inf, flags;
   dbuf<int32_t> sig_code, pk_code, job_code, job_result, set_code;
   dbuf<g1a> rpk_aff;
+  dbuf<uint32_t> chunk_off, chunk_set;
+  dbuf<g1j> pk_part;
   dbuf<g2j> rsig;
   dbuf<fp12_t> f_set, f_job, f_batch, f_part;
   dbuf<uint32_t> set_job, s_inf;
@@ -142,7 +144,7 @@ int bgv_close(bgv_ctx* c) {
   c->scalars.release(); c->raw_conv.release();
   c->sig_aff.release(); c->h_aff.release(); c->sig_inf.release(); c->flags.release();
   c->sig_code.release(); c->pk_code.release(); c->job_code.release(); c->job_result.release(); c->set_code.release();
-  c->rpk_aff.release(); c->rsig.release(); c->f_set.release(); c->f_job.release(); c->f_batch.release(); c->f_part.release();
+  c->rpk_aff.release(); c->chunk_off.release(); c->chunk_set.release(); c->pk_part.release(); c->rsig.release(); c->f_set.release(); c->f_job.release(); c->f_batch.release(); c->f_part.release();
   c->set_job.release(); c->s_inf.release(); c->s_aff.release();
   c->mb_fp.release(); c->mb_u64.release();
   (void)hipStreamDestroy(c->st);
@@ -286,6 +288,14 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, std::vector<uin
     launch_raw_pks(c->st, b->raw_pks, c->raw_conv.p, b->n_raw);
     d.raw_pks = c->raw_conv.p;
   }
+  // grid bound of the chunked pubkey gather: sum ceil(k_i/32) <= total/32 + n
+  uint32_t total = 0;
+  if (!b->on_device) total = b->pk_offsets[n];
+  else if (n) {
+    HIPCHK(hipMemcpyAsync(&total, b->pk_offsets + n, 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+  }
+  d.chunk_bound = total / 32 + n;
   if (b->scalars && !b->on_device) {
     if (int r = stage_in(c, c->scalars, b->scalars, (size_t)n, d.scalars)) return r;
   } else if (b->scalars) {
@@ -298,9 +308,14 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, std::vector<uin
   return 0;
 }
 
-static int work_alloc(bgv_ctx* c, uint32_t n, uint32_t J, dev_work& w) {
+static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
+  const uint32_t n = d.n_sets, J = d.n_jobs;
   const size_t ns = n ? n : 1, nj = J ? J : 1;
   int r = 0;
+  if ((r = c->chunk_off.ensure(ns + 1)) || (r = c->chunk_set.ensure((size_t)d.chunk_bound + 1)) ||
+      (r = c->pk_part.ensure((size_t)d.chunk_bound + 1)))
+    return r;
+  w.chunk_off = c->chunk_off.p; w.chunk_set = c->chunk_set.p; w.pk_part = c->pk_part.p;
   if ((r = c->sig_aff.ensure(ns)) || (r = c->h_aff.ensure(ns)) || (r = c->sig_inf.ensure(ns)) ||
       (r = c->sig_code.ensure(ns)) || (r = c->pk_code.ensure(ns)) || (r = c->rpk_aff.ensure(ns)) ||
       (r = c->rsig.ensure(ns)) || (r = c->f_set.ensure(ns + nj)) || (r = c->set_code.ensure(ns)) ||
@@ -334,7 +349,7 @@ int bgv_verify(bgv_ctx* c, const bgv_batch* b, int32_t* job_result, int32_t* set
   std::vector<uint64_t> scal;
   if (int r = prepare(c, b, d, scal, true)) return r;
   dev_work w;
-  if (int r = work_alloc(c, d.n_sets, d.n_jobs, w)) return r;
+  if (int r = work_alloc(c, d, w)) return r;
   if (int r = run_stages(c, d, w, 0, ST_COUNT)) return r;
   if (d.n_jobs) HIPCHK(hipMemcpyAsync(job_result, w.job_result, (size_t)d.n_jobs * 4, hipMemcpyDeviceToHost, c->st));
   if (set_code && d.n_sets) HIPCHK(hipMemcpyAsync(set_code, w.set_code, (size_t)d.n_sets * 4, hipMemcpyDeviceToHost, c->st));
@@ -384,7 +399,7 @@ int bgv_partial(bgv_ctx* c, const bgv_batch* b, uint8_t* miller576, int32_t* set
   std::vector<uint64_t> scal;
   if (int r = prepare(c, b, d, scal, true)) return r;
   dev_work w;
-  if (int r = work_alloc(c, d.n_sets, d.n_jobs, w)) return r;
+  if (int r = work_alloc(c, d, w)) return r;
   if (int r = run_stages(c, d, w, ST_SIG, ST_BATCH_FINAL)) return r;
   launch_stage(c->st, ST_SET_CODES, d, w);
   fp12_t f;

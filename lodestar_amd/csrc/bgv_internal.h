@@ -15,7 +15,8 @@ enum : int32_t {
 // indexed by set (or job); see include/bgv.h bgv_batch for their meaning.
 struct dev_batch {
   uint32_t n_sets, n_jobs, n_raw, table_n;
-  uint32_t span_log2;  // per-job reduction tree covers 2^span_log2 sets
+  uint32_t span_log2;    // per-job reduction tree covers 2^span_log2 sets
+  uint32_t chunk_bound;  // upper bound of pubkey chunks (grid of k_pk_chunk)
   const uint32_t* job_off;
   const uint32_t* pk_off;
   const uint32_t* pk_idx;
@@ -33,6 +34,9 @@ struct dev_work {
   uint32_t* sig_inf;  // signature is the identity
   int32_t* sig_code;  // parse / subgroup outcome
   g2a* h_aff;         // H(m)
+  uint32_t* chunk_off;  // [n_sets + 1] scan of per-set pubkey chunk counts
+  uint32_t* chunk_set;  // set of every chunk
+  g1j* pk_part;         // per-chunk partial sums
   g1a* rpk_aff;       // [r_i] aggregated pubkey, affine
   int32_t* pk_code;
   g2j* rsig;          // [r_i] sigma_i

@@ -21,6 +21,7 @@
 //   k_job_final   per-job final exponentiation only if the batch check failed
 //                 (the worker's per-job retry, multithread/worker.ts:74-85)
 #include "bgv_internal.h"
+#include "fp12_wave.h"
 
 namespace bgv {
 
@@ -131,10 +132,56 @@ __global__ void BGV_BULK k_hash(dev_batch b, dev_work w) {
 }
 
 // ------------------------------------------------------------------- k_pk
-__global__ void BGV_BULK k_pk(dev_batch b, dev_work w) {
+// PublicKey.aggregate as a balanced gather: every set's index list is cut
+// into chunks of PK_CHUNK keys (a 512-key sync-committee set is 16 chunks,
+// a 128-key attestation 4, a single 1) so lanes of one wave do equal work;
+// chunk offsets come from a device scan.  Then one lane per set folds its
+// chunk sums, applies the batch scalar r_i and converts to affine.
+constexpr uint32_t PK_CHUNK = 32;
+
+__global__ void BGV_BULK k_chunk_count(dev_batch b, dev_work w) {
   const uint32_t i = gtid();
   if (i >= b.n_sets) return;
-  const uint32_t beg = b.pk_off[i], end = b.pk_off[i + 1];
+  const uint32_t k = b.pk_off[i + 1] - b.pk_off[i];
+  w.chunk_off[i] = (k + PK_CHUNK - 1) / PK_CHUNK;
+}
+
+// exclusive scan of chunk_off[0..n) in place, total at [n]; one workgroup
+__global__ void __launch_bounds__(1024) k_chunk_scan(dev_batch b, dev_work w) {
+  __shared__ uint32_t part[1024];
+  const uint32_t t = threadIdx.x, n = b.n_sets;
+  const uint32_t per = (n + 1023) / 1024, beg = t * per, end = min(n, beg + per);
+  uint32_t s = 0;
+  for (uint32_t i = beg; i < end; i++) s += w.chunk_off[i];
+  part[t] = s;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d *= 2) {
+    const uint32_t v = t >= d ? part[t - d] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - s;  // exclusive prefix of this thread's segment
+  for (uint32_t i = beg; i < end; i++) {
+    const uint32_t c = w.chunk_off[i];
+    w.chunk_off[i] = run;
+    run += c;
+  }
+  if (t == 1023) w.chunk_off[n] = part[1023];
+}
+
+__global__ void BGV_BULK k_chunk_set(dev_batch b, dev_work w) {
+  const uint32_t i = gtid();
+  if (i >= b.n_sets) return;
+  for (uint32_t c = w.chunk_off[i]; c < w.chunk_off[i + 1]; c++) w.chunk_set[c] = i;
+}
+
+__global__ void BGV_BULK k_pk_chunk(dev_batch b, dev_work w) {
+  const uint32_t g = gtid();
+  if (g >= w.chunk_off[b.n_sets]) return;
+  const uint32_t i = w.chunk_set[g];
+  const uint32_t beg = b.pk_off[i] + (g - w.chunk_off[i]) * PK_CHUNK;
+  const uint32_t end = min(beg + PK_CHUNK, b.pk_off[i + 1]);
   g1j acc;
   jac_set_inf(acc);
   bool range_err = false;
@@ -143,6 +190,25 @@ __global__ void BGV_BULK k_pk(dev_batch b, dev_work w) {
     load_pk(p, b, b.pk_idx[k], range_err);
     if (g1a_is_zero(p)) continue;  // infinity entry adds nothing
     jac_add_aff(acc, acc, p);
+  }
+  if (range_err) {  // marker (X, Y, Z) = (0, 1, 1): not on E1, never produced by point additions
+    fp_set_zero(acc.x);
+    acc.y = FP_ONE;
+    acc.z = FP_ONE;
+  }
+  w.pk_part[g] = acc;
+}
+
+__global__ void BGV_BULK k_pk(dev_batch b, dev_work w) {
+  const uint32_t i = gtid();
+  if (i >= b.n_sets) return;
+  g1j acc;
+  jac_set_inf(acc);
+  bool range_err = false;
+  for (uint32_t c = w.chunk_off[i]; c < w.chunk_off[i + 1]; c++) {
+    const g1j p = w.pk_part[c];
+    if (!jac_is_inf(p) && fp_is_zero(p.x)) range_err = true;
+    jac_add(acc, acc, p);
   }
   int32_t code = C_OK;
   if (range_err) code = C_INDEX_RANGE;
@@ -153,7 +219,8 @@ __global__ void BGV_BULK k_pk(dev_batch b, dev_work w) {
     jac_mul_u64(rp, acc, b.scalars[i]);
     jac_to_aff(out, rp);
   } else {
-    fp_set_zero(out.x); fp_set_zero(out.y);
+    fp_set_zero(out.x);
+    fp_set_zero(out.y);
   }
   w.rpk_aff[i] = out;
   w.pk_code[i] = code;
@@ -284,15 +351,15 @@ __global__ void BGV_BULK k_batch_level(dev_batch b, dev_work w, uint32_t s) {
   w.f_batch[j] = a;
 }
 
+// the whole-batch check: ONE final exponentiation, wave-cooperative (fp12_wave.h)
 __global__ void BGV_BULK k_batch_final(dev_batch b, dev_work w) {
-  if (threadIdx.x != 0) return;
+  __shared__ wscratch s;
   if (b.n_jobs == 0) {
-    w.flags[0] = 0u;
+    if (threadIdx.x == 0) w.flags[0] = 0u;
     return;
   }
-  fp12_t r;
-  fp12_final_exp(r, w.f_batch[0]);
-  w.flags[0] = fp12_is_one(r) ? 1u : 0u;
+  const bool one = w_final_exp_is_one(w.f_batch[0], &s);
+  if (threadIdx.x == 0) w.flags[0] = one ? 1u : 0u;
 }
 
 // ------------------------------------------------------------ k_job_final
@@ -323,13 +390,15 @@ __global__ void BGV_BULK k_set_codes(dev_batch b, dev_work w) {
 
 // ------------------------------------------------- multi-GPU combination
 __global__ void BGV_BULK k_combine_final(const fp12_t* parts, uint32_t n, uint32_t* flag) {
-  if (threadIdx.x != 0) return;
-  fp12_t g;
-  fp12_one(g);
-  for (uint32_t k = 0; k < n; k++) fp12_mul(g, g, parts[k]);
-  fp12_t r;
-  fp12_final_exp(r, g);
-  flag[0] = fp12_is_one(r) ? 1u : 0u;
+  __shared__ wscratch s;
+  __shared__ fp12_t g;
+  if (threadIdx.x == 0) {
+    fp12_one(g);
+    for (uint32_t k = 0; k < n; k++) fp12_mul(g, g, parts[k]);
+  }
+  __syncthreads();
+  const bool one = w_final_exp_is_one(g, &s);
+  if (threadIdx.x == 0) flag[0] = one ? 1u : 0u;
 }
 
 // Montgomery <-> plain limbs for Fp12 values crossing the host boundary
@@ -513,7 +582,13 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
   switch (stage) {
     case ST_SIG: BGV_LAUNCH(k_sig, b.n_sets, b, w); break;
     case ST_HASH: BGV_LAUNCH(k_hash, b.n_sets, b, w); break;
-    case ST_PK: BGV_LAUNCH(k_pk, b.n_sets, b, w); break;
+    case ST_PK:
+      BGV_LAUNCH(k_chunk_count, b.n_sets, b, w);
+      if (b.n_sets) hipLaunchKernelGGL(k_chunk_scan, dim3(1), dim3(1024), 0, st, b, w);
+      BGV_LAUNCH(k_chunk_set, b.n_sets, b, w);
+      BGV_LAUNCH(k_pk_chunk, b.chunk_bound, b, w);
+      BGV_LAUNCH(k_pk, b.n_sets, b, w);
+      break;
     case ST_SIG_SCALE: BGV_LAUNCH(k_sig_scale, b.n_sets, b, w); break;
     case ST_S_TREE:
       BGV_LAUNCH(k_set_job, b.n_jobs, b, w);
