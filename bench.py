@@ -136,6 +136,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from lodestar_amd import native
+    from lodestar_amd.dist import verify_sharded
 
     d = native.Device(local)
     t0 = time.time()
@@ -158,12 +159,8 @@ def main():
         if world == 1:
             jr, _ = d.verify(darr, on_device=True, want_set_codes=False)
             return bool((jr == 1).all())
-        part, _, ok = d.partial(darr, on_device=True)
-        t = torch.frombuffer(bytearray(part), dtype=torch.uint8).to(dev)
-        parts = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(parts, t)
-        allp = [p.cpu().numpy().tobytes() for p in parts]
-        return ok and d.combine_final(allp)
+        valid, ok = verify_sharded(d, darr, dist, device=dev, on_device=True)
+        return ok and valid
 
     for _ in range(args.warmup):
         assert step(), "warm-up batch did not verify"

@@ -423,6 +423,58 @@ class BlsGpuVerifier:
         return out
 
 
+async def reject_first_invalid_resolve_all_valid(is_valid_awaitables) -> dict:
+    """chain/blocks/verifyBlocksSignatures.ts:69-89: resolves {"allValid": False,
+    "index": i} at the first False to arrive, {"allValid": True} when all are
+    True; an exception rejects."""
+    tasks = [asyncio.ensure_future(a) for a in is_valid_awaitables]
+    idx = {t: i for i, t in enumerate(tasks)}
+    pending = set(tasks)
+    try:
+        while pending:
+            done, pending = await asyncio.wait(pending, return_when=asyncio.FIRST_COMPLETED)
+            for t in sorted(done, key=lambda t: idx[t]):
+                if not t.result():
+                    return {"allValid": False, "index": idx[t]}
+        return {"allValid": True}
+    finally:
+        for t in pending:
+            t.cancel()
+
+
+async def verify_blocks_signatures(bls: "BlsGpuVerifier", blocks_sets: list[list[ISignatureSet]],
+                                   coalesce: bool = True) -> dict:
+    """verifyBlocksSignatures (chain/blocks/verifyBlocksSignatures.ts:16-60) for
+    a segment of blocks.  coalesce=False issues one verifySignatureSets per
+    block exactly like the reference; coalesce=True sends
+    the whole segment as ONE device batch with one job per block (each block
+    <= 128 sets is exactly one reference job), so the per-block verdicts come
+    from a single whole-segment pairing check plus per-block checks only on
+    failure.  Verdict semantics are the same; with every block result
+    arriving at once, the first invalid block by index is reported."""
+    if not coalesce:
+        return await reject_first_invalid_resolve_all_valid([bls.verify_signature_sets(s) for s in blocks_sets])
+    jobs = []
+    owner = []
+    for b, sets in enumerate(blocks_sets):
+        for s in sets:
+            if s.type == SignatureSetType.aggregate and len(s.pubkeys) == 0:
+                raise BlsError("EMPTY_AGGREGATE_ARRAY")
+        for chunk in chunkify_maximize_chunk_size(sets, MAX_SIGNATURE_SETS_PER_JOB):
+            jobs.append(chunk)
+            owner.append(b)
+    res = await asyncio.get_running_loop().run_in_executor(bls._exec, bls._run_device_batch, jobs)
+    ok = [True] * len(blocks_sets)
+    for b, r in zip(owner, res):
+        if isinstance(r, Exception):
+            raise r
+        ok[b] = ok[b] and r
+    for b, v in enumerate(ok):
+        if not v:
+            return {"allValid": False, "index": b}
+    return {"allValid": True}
+
+
 def _new_metrics() -> dict:
     """Counterparts of lodestar_bls_thread_pool_* (metrics/metrics/lodestar.ts:350-430)."""
     return {

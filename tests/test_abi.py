@@ -1,0 +1,80 @@
+"""The C-ABI library: builds for gfx950, loads without a GPU, exports every
+symbol include/bgv.h declares, and its struct layout matches the ctypes
+mirror.  No compute calls here (no GPU in the build container)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "bgv.h")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from tools import build
+    build.build()
+    from lodestar_amd import native
+    return native.load_library()
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(bgv_\w+)\s*\(", src, re.M)))
+
+
+def test_every_declared_symbol_is_exported(lib):
+    names = declared_functions()
+    assert len(names) >= 16
+    out = subprocess.check_output(["nm", "-D", "--defined-only", os.path.join(ROOT, "lodestar_amd", "libbgv.so")]).decode()
+    exported = set(re.findall(r" T (bgv_\w+)", out))
+    assert set(names) <= exported, set(names) - exported
+    from lodestar_amd import native
+    assert set(native.EXPORTS) == set(names)
+
+
+def test_struct_layout_matches_ctypes(tmp_path):
+    from lodestar_amd import native
+    c = tmp_path / "layout.c"
+    fields_b = [f for f, _ in native.BgvBatch._fields_]
+    fields_s = [f for f, _ in native.BgvStats._fields_]
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "bgv.h"', "int main(void){"]
+    lines.append('printf("%zu %zu\\n", sizeof(bgv_batch), sizeof(bgv_stats));')
+    for f in fields_b:
+        lines.append(f'printf("%zu\\n", offsetof(bgv_batch, {f}));')
+    for f in fields_s:
+        lines.append(f'printf("%zu\\n", offsetof(bgv_stats, {f}));')
+    lines.append("return 0;}")
+    c.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(c), "-o", str(exe)])
+    vals = subprocess.check_output([str(exe)]).decode().split()
+    assert int(vals[0]) == ctypes.sizeof(native.BgvBatch)
+    assert int(vals[1]) == ctypes.sizeof(native.BgvStats)
+    offs = [int(v) for v in vals[2:]]
+    assert offs[: len(fields_b)] == [getattr(native.BgvBatch, f).offset for f in fields_b]
+    assert offs[len(fields_b):] == [getattr(native.BgvStats, f).offset for f in fields_s]
+
+
+def test_metadata_and_no_silent_fallback(lib):
+    from lodestar_amd import native
+    assert lib.bgv_abi_version() == 1
+    assert lib.bgv_set_code_name(8) == b"BLST_INVALID_SIZE"
+    assert lib.bgv_set_code_name(3) == b"BLST_POINT_NOT_IN_GROUP"
+    assert lib.bgv_stage_name(5) == b"miller_loop"
+    try:
+        import torch
+        has_gpu = torch.cuda.is_available()
+    except Exception:
+        has_gpu = False
+    if not has_gpu:
+        # the product path fails loudly without a HIP device: no CPU fallback
+        with pytest.raises(native.BgvNativeError):
+            native.Device(0)
+
+
+def test_gfx950_code_object_present(lib):
+    blob = open(os.path.join(ROOT, "lodestar_amd", "libbgv.so"), "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob  # the fat binary carries a gfx950 code object

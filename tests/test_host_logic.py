@@ -1,0 +1,92 @@
+"""Host logic of the IBlsVerifier mirror (no GPU): chunking, batch encoding,
+error strings, block-level verdict ordering and job sharding."""
+import asyncio
+
+import numpy as np
+import pytest
+
+from lodestar_amd import verifier as V
+from lodestar_amd.dist import shard_jobs
+
+
+def test_chunkify_matches_reference_unit_test():
+    # packages/beacon-node/test/unit/chain/bls/utils.test.ts (minPerChunk = 3)
+    expected = [
+        [[0]], [[0, 1]], [[0, 1, 2]], [[0, 1, 2, 3]], [[0, 1, 2, 3, 4]],
+        [[0, 1, 2], [3, 4, 5]], [[0, 1, 2, 3], [4, 5, 6]], [[0, 1, 2, 3], [4, 5, 6, 7]],
+    ]
+    for i, exp in enumerate(expected):
+        assert V.chunkify_maximize_chunk_size(list(range(i + 1)), 3) == exp
+    assert V.chunkify_maximize_chunk_size([], 128) == [[]]
+
+
+def test_chunkify_pool_sizes():
+    for n in (1, 127, 128, 255, 256, 257, 1000, 8000):
+        chunks = V.chunkify_maximize_chunk_size(list(range(n)), 128)
+        assert [x for c in chunks for x in c] == list(range(n))
+        if n >= 256:  # floor(n / 128) chunks of ceil(n / count) (the last one may be shorter)
+            assert len(chunks) == n // 128 or len(chunks) == -(-n // -(-n // (n // 128)))
+            assert max(len(c) for c in chunks) == -(-n // (n // 128))
+
+
+def _set(idxs, root=b"\x01" * 32, sig=b"\xaa" * 96):
+    pks = [V.PublicKey(index=i) for i in idxs]
+    if len(pks) == 1:
+        return V.create_single_signature_set_from_components(pks[0], root, sig)
+    return V.create_aggregate_signature_set_from_components(pks, root, sig)
+
+
+def test_encode_jobs_layout():
+    raw = V.PublicKey.from_bytes(b"\x11" * 96)
+    jobs = [[_set([5]), _set([1, 2, 3])], [V.create_single_signature_set_from_components(raw, b"\x02" * 32, b"\x00" * 32)]]
+    a = V.encode_jobs(jobs)
+    assert a["n_sets"] == 3 and a["n_jobs"] == 2
+    assert a["job_offsets"].tolist() == [0, 2, 3]
+    assert a["pk_offsets"].tolist() == [0, 1, 4, 5]
+    assert a["pk_indices"].tolist() == [5, 1, 2, 3, 0x80000000]
+    assert a["n_raw"] == 1 and a["raw_pks"].tobytes() == b"\x11" * 96
+    assert a["sig_len"].tolist() == [96, 96, 32]
+    assert (a["sigs"][2] == 0).all()  # a 32-byte signature travels as its length only
+
+
+def test_empty_aggregate_rejects():
+    with pytest.raises(V.BlsError, match="EMPTY_AGGREGATE_ARRAY"):
+        V.encode_jobs([[V.create_aggregate_signature_set_from_components([], bytes(32), bytes(96))]])
+
+
+def test_error_strings_match_reference_tests():
+    assert "BLST_INVALID_SIZE" in str(V.error_for_code(8))          # multithread.test.ts:97
+    assert "BLST_ERROR" in str(V.error_for_code(3))                  # spec/general/bls.ts:37
+    assert str(V.error_for_code(10)) == "Empty signature set"        # maybeBatch.ts:30
+    with pytest.raises(V.BlsError, match="BLST_INVALID_SIZE"):
+        V.PublicKey.from_bytes(b"\x00" * 10)
+
+
+def test_reject_first_invalid_resolve_all_valid():
+    # test/unit/chain/blocks/rejectFirstInvalidResolveAllValid.test.ts
+    async def run():
+        loop = asyncio.get_running_loop()
+        futs = [loop.create_future() for _ in range(3)]
+        task = asyncio.ensure_future(V.reject_first_invalid_resolve_all_valid(futs))
+        await asyncio.sleep(0)
+        futs[2].set_result(True)
+        await asyncio.sleep(0)
+        futs[1].set_result(False)
+        res = await task
+        assert res == {"allValid": False, "index": 1}
+        futs2 = [loop.create_future() for _ in range(3)]
+        task2 = asyncio.ensure_future(V.reject_first_invalid_resolve_all_valid(futs2))
+        for f in futs2:
+            f.set_result(True)
+        assert await task2 == {"allValid": True}
+    asyncio.run(run())
+
+
+def test_shard_jobs_balanced_and_complete():
+    sizes = [98] * 1024 + [1, 5, 128]
+    for world in (1, 2, 4, 8):
+        shards = shard_jobs(sizes, world)
+        flat = sorted(j for s in shards for j in s)
+        assert flat == list(range(len(sizes)))
+        loads = [sum(sizes[j] for j in s) for s in shards]
+        assert max(loads) - min(loads) <= 128
