@@ -106,10 +106,24 @@ BGV_HD void fp_neg(fp_t& r, const fp_t& a) {
 #ifdef BGV_COUNT_OPS
 extern unsigned long long bgv_fpmul_count;  // host op-count build only (tools/opcount.cpp)
 #endif
+BGV_HD void fp_mul28(fp_t& r, const fp_t& a, const fp_t& b);
+BGV_HD void fp_mul32(fp_t& r, const fp_t& a, const fp_t& b);
+#ifndef BGV_FPMUL28
+#define BGV_FPMUL28 1
+#endif
 BGV_HD void fp_mul(fp_t& r, const fp_t& a, const fp_t& b) {
 #ifdef BGV_COUNT_OPS
   bgv_fpmul_count++;
 #endif
+#if BGV_FPMUL28
+  fp_mul28(r, a, b);
+#else
+  fp_mul32(r, a, b);
+#endif
+}
+
+// 12 x 32-bit CIOS (operand scanning)
+BGV_HD void fp_mul32(fp_t& r, const fp_t& a, const fp_t& b) {
   uint32_t t[NL];
 #pragma unroll
   for (int i = 0; i < NL; i++) t[i] = 0;
@@ -137,6 +151,86 @@ BGV_HD void fp_mul(fp_t& r, const fp_t& a, const fp_t& b) {
 #pragma unroll
   for (int i = 0; i < NL; i++) s.l[i] = t[i];
   fp_reduce_once(r, s);
+}
+
+// ---- product-scanning variant on 28-bit digits -------------------------
+// The 12 x 32-bit CIOS above keeps every partial product inside a carry
+// chain, so hipcc spends ~1,000 v_mov / v_lshl_add_u64 per product building
+// 64-bit addends.  Here both operands are split into 14 digits of 28 bits;
+// a digit product is < 2^56, so every column of the schoolbook and of the
+// Montgomery reduction accumulates in a 64-bit register with one
+// v_mad_u64_u32 per digit pair and no carries until the end (27
+// independent columns: high ILP).  The representation outside stays
+// 12 x 32-bit Montgomery with R = 2^384: `a` enters shifted by 8 bits, so the
+// 2^-392 of the 28-bit reduction yields a*b*2^-384.  Output < 2p, then one
+// conditional subtraction.
+BGV_CONST uint32_t P28[14] = {0xfffaaabu, 0xfefffffu, 0x3ffffb9u, 0xfffeb15u, 0x6241eabu, 0xa0f6b0fu, 0xf6730d2u,
+                              0xf38512bu, 0x4774b84u, 0x4bacd76u, 0xba7b643u, 0xe69a4b1u, 0x1ea397fu, 0x001a011u};
+constexpr uint32_t P28_INV = 0xffcfffdu;  // -p^-1 mod 2^28
+constexpr uint32_t M28 = 0x0fffffffu;
+
+// digit k of (a << shift): bits [28k - shift, 28k - shift + 28) of a
+template <int SHIFT>
+BGV_HD void unpack28(uint32_t d[14], const fp_t& a) {
+#pragma unroll
+  for (int k = 0; k < 14; k++) {
+    const int pos = 28 * k - SHIFT;
+    uint32_t v;
+    if (pos < 0) {
+      v = a.l[0] << (-pos);
+    } else {
+      const int w = pos >> 5, sh = pos & 31;
+      const uint32_t lo = w < NL ? a.l[w] : 0u;
+      const uint32_t hi = (w + 1) < NL ? a.l[w + 1] : 0u;
+      v = sh ? ((lo >> sh) | (hi << (32 - sh))) : lo;
+    }
+    d[k] = v & M28;
+  }
+}
+
+BGV_HD void pack28(fp_t& r, const uint32_t d[14]) {
+#pragma unroll
+  for (int m = 0; m < NL; m++) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 14; k++) {
+      const int lo_bit = 28 * k, rel = lo_bit - 32 * m;  // digit k starts at bit rel of limb m
+      if (rel >= 32 || rel <= -28) continue;
+      v |= rel >= 0 ? (d[k] << rel) : (d[k] >> (-rel));
+    }
+    r.l[m] = v;
+  }
+}
+
+BGV_HD void fp_mul28(fp_t& r, const fp_t& a, const fp_t& b) {
+  uint32_t A[14], B[14];
+  unpack28<8>(A, a);
+  unpack28<0>(B, b);
+  uint64_t acc[28];
+#pragma unroll
+  for (int k = 0; k < 28; k++) acc[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++)
+#pragma unroll
+    for (int j = 0; j < 14; j++) acc[i + j] += (uint64_t)A[i] * B[j];
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    const uint32_t m = ((uint32_t)acc[i] * P28_INV) & M28;
+#pragma unroll
+    for (int j = 0; j < 14; j++) acc[i + j] += (uint64_t)m * P28[j];
+    acc[i + 1] += acc[i] >> 28;
+  }
+  uint32_t d[14];
+  uint64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 14; k++) {
+    const uint64_t v = acc[14 + k] + c;
+    d[k] = (uint32_t)v & M28;
+    c = v >> 28;
+  }
+  fp_t t;
+  pack28(t, d);
+  fp_reduce_once(r, t);
 }
 
 BGV_HD void fp_sqr(fp_t& r, const fp_t& a) { fp_mul(r, a, a); }

@@ -9,7 +9,8 @@ from oracle import bls12_381 as B
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "native", "hostcheck.cpp")
-LIB = os.path.join(HERE, "native", "libhostcheck.so")
+DEFS = [d for d in os.environ.get("BGV_HOST_DEFS", "").split() if d]  # e.g. "-DBGV_FPMUL28=1"
+LIB = os.path.join(HERE, "native", "libhostcheck%s.so" % ("_" + "_".join(x.strip("-D").replace("=", "") for x in DEFS) if DEFS else ""))
 CSRC = os.path.join(os.path.dirname(HERE), "lodestar_amd", "csrc")
 
 
@@ -23,7 +24,7 @@ def _stale():
 
 def load():
     if _stale():
-        subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", LIB, SRC])
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC"] + DEFS + ["-o", LIB, SRC])
     lib = ctypes.CDLL(LIB)
     lib.hc_g2_mul_u64.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
     lib.hc_g1_mul_u64.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]

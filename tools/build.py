@@ -52,7 +52,11 @@ def build(force=False, verbose=False, lib=LIB, defines=()):
 
 
 if __name__ == "__main__":
-    if "--variants" in sys.argv:  # occupancy experiment builds
+    if "--variant" in sys.argv:  # --variant NAME DEF [DEF ...]
+        k = sys.argv.index("--variant")
+        name, defs = sys.argv[k + 1], sys.argv[k + 2:]
+        print(build(force=True, lib=LIB.replace(".so", f"_{name}.so"), defines=defs))
+    elif "--variants" in sys.argv:  # occupancy experiment builds
         for w in (1, 2, 4):
             print(build(force=True, lib=LIB.replace(".so", f"_w{w}.so"), defines=[f"BGV_WAVES={w}"]))
     else:
