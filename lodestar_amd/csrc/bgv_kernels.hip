@@ -216,7 +216,7 @@ __global__ void BGV_BULK k_pk(dev_batch b, dev_work w) {
   g1a out;
   if (code == C_OK) {
     g1j rp;
-    jac_mul_u64(rp, acc, b.scalars[i]);
+    jac_mul_u64_w4(rp, acc, b.scalars[i]);
     jac_to_aff(out, rp);
   } else {
     fp_set_zero(out.x);
@@ -236,7 +236,7 @@ __global__ void BGV_BULK k_sig_scale(dev_batch b, dev_work w) {
   } else {
     g2j s;
     jac_from_aff(s, w.sig_aff[i]);
-    jac_mul_u64(r, s, b.scalars[i]);
+    jac_mul_u64_w4(r, s, b.scalars[i]);
   }
   w.rsig[i] = r;
 }

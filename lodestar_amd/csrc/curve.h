@@ -178,6 +178,31 @@ template <class F> BGV_NI void jac_mul_u64(jac_t<F>& r, const jac_t<F>& p, uint6
   r = acc;
 }
 
+// [k]P for a RANDOM 64-bit scalar (the batch multipliers r_i), fixed 4-bit
+// window with a per-lane table {O, P, .., 15P}.  Double-and-add branches on
+// each lane's own bits, so a wave executes the addition at almost every bit
+// (64 dbl + ~64 add); here every lane runs the same 60 dbl + 15 add + 14
+// table steps.
+template <class F> BGV_NI void jac_mul_u64_w4(jac_t<F>& r, const jac_t<F>& p, uint64_t k) {
+  jac_t<F> tab[16];
+  jac_set_inf(tab[0]);
+  tab[1] = p;
+  jac_dbl(tab[2], p);
+#pragma unroll 1
+  for (int i = 3; i < 16; i++) jac_add(tab[i], tab[i - 1], p);
+  jac_t<F> acc = tab[(k >> 60) & 15];
+#pragma unroll 1
+  for (int w = 14; w >= 0; w--) {
+    jac_dbl(acc, acc);
+    jac_dbl(acc, acc);
+    jac_dbl(acc, acc);
+    jac_dbl(acc, acc);
+    const jac_t<F> t = tab[(k >> (4 * w)) & 15];
+    jac_add(acc, acc, t);
+  }
+  r = acc;
+}
+
 // [|x|]P for the BLS parameter (Hamming weight 6)
 template <class F> BGV_NI void jac_mul_abs_x(jac_t<F>& r, const jac_t<F>& p) {
   jac_t<F> acc = p;

@@ -28,6 +28,8 @@ def load():
     lib = ctypes.CDLL(LIB)
     lib.hc_g2_mul_u64.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
     lib.hc_g1_mul_u64.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+    lib.hc_g2_mul_u64_w4.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+    lib.hc_g1_mul_u64_w4.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
     return lib
 
 

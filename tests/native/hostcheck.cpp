@@ -64,6 +64,8 @@ int hc_g1_decompress(const uint8_t* in48, uint8_t* out96, int* inf) {
 }
 int hc_g2_in_subgroup(const uint8_t* aff192) { g2a a; get_g2a(a, aff192); g2j j; jac_from_aff(j, a); return g2_in_subgroup(j); }
 int hc_g2_mul_u64(const uint8_t* aff192, uint64_t k, uint8_t* out192) { g2a a; get_g2a(a, aff192); g2j j, r; jac_from_aff(j, a); jac_mul_u64(r, j, k); return put_g2j(out192, r); }
+int hc_g2_mul_u64_w4(const uint8_t* aff192, uint64_t k, uint8_t* out192) { g2a a; get_g2a(a, aff192); g2j j, r; jac_from_aff(j, a); jac_mul_u64_w4(r, j, k); return put_g2j(out192, r); }
+int hc_g1_mul_u64_w4(const uint8_t* aff96, uint64_t k, uint8_t* out96) { g1a a; get_g1a(a, aff96); g1j j, r; jac_from_aff(j, a); jac_mul_u64_w4(r, j, k); return put_g1j(out96, r); }
 int hc_g1_mul_u64(const uint8_t* aff96, uint64_t k, uint8_t* out96) { g1a a; get_g1a(a, aff96); g1j j, r; jac_from_aff(j, a); jac_mul_u64(r, j, k); return put_g1j(out96, r); }
 int hc_g2_add(const uint8_t* a192, const uint8_t* b192, uint8_t* out192) {
   g2a a, b; get_g2a(a, a192); get_g2a(b, b192); g2j ja, jb, r; jac_from_aff(ja, a); jac_from_aff(jb, b); jac_add(r, ja, jb); return put_g2j(out192, r);

@@ -177,6 +177,12 @@ def test_point_arith():
     G = B.E1.mul(B.G1, 99)
     lib.hc_g1_mul_u64(H.g1_b(G), k, o1)
     assert B.E1.eq(H.b_g1(o1.raw), B.E1.mul(G, k))
+    # fixed-window variant used by the kernels for the random batch scalars
+    for kk in (1, 2, 15, 16, 0x10, 0xF000000000000000, k, 2**64 - 1, 0x8000000000000001):
+        lib.hc_g2_mul_u64_w4(H.g2_b(P), kk, o)
+        assert B.E2.eq(H.b_g2(o.raw), B.E2.mul(P, kk)), hex(kk)
+        lib.hc_g1_mul_u64_w4(H.g1_b(G), kk, o1)
+        assert B.E1.eq(H.b_g1(o1.raw), B.E1.mul(G, kk)), hex(kk)
     pts = [B.E1.mul(B.G1, i + 3) for i in range(5)]
     blob = b"".join(H.g1_b(p) for p in pts)
     lib.hc_g1_sum(blob, 5, o1)

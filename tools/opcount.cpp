@@ -44,10 +44,10 @@ int main(int argc, char** argv) {
     for (int i = 1; i < 64; i++) jac_add_aff(acc, acc, pts[i]);
     pk_add_c += (double)bgv_fpmul_count / 63.0;
     bgv_fpmul_count = 0;
-    g1j rp; jac_mul_u64(rp, acc, sc); g1a rpa; jac_to_aff(rpa, rp);
+    g1j rp; jac_mul_u64_w4(rp, acc, sc); g1a rpa; jac_to_aff(rpa, rp);
     pk_fix_c += bgv_fpmul_count;
     bgv_fpmul_count = 0;
-    g2j s2; jac_from_aff(s2, a); g2j rs; jac_mul_u64(rs, s2, sc);
+    g2j s2; jac_from_aff(s2, a); g2j rs; jac_mul_u64_w4(rs, s2, sc);
     sig_scale_c += bgv_fpmul_count;
     bgv_fpmul_count = 0;
     g2j t2 = rs; jac_add(t2, t2, rs); jac_add(t2, t2, s2);
