@@ -81,7 +81,7 @@ struct bgv_ctx {
   dbuf<g1j> pk_part;
   dbuf<g2j> rsig;
   dbuf<fp12_t> f_set, f_job, f_batch, f_part;
-  dbuf<uint32_t> set_job, s_inf;
+  dbuf<uint32_t> set_job, s_inf, item_off, item_job;
   dbuf<g2a> s_aff;
   // microbench scratch
   dbuf<fp_t> mb_fp;
@@ -145,7 +145,7 @@ int bgv_close(bgv_ctx* c) {
   c->sig_aff.release(); c->h_aff.release(); c->sig_inf.release(); c->flags.release();
   c->sig_code.release(); c->pk_code.release(); c->job_code.release(); c->job_result.release(); c->set_code.release();
   c->rpk_aff.release(); c->chunk_off.release(); c->chunk_set.release(); c->pk_part.release(); c->rsig.release(); c->f_set.release(); c->f_job.release(); c->f_batch.release(); c->f_part.release();
-  c->set_job.release(); c->s_inf.release(); c->s_aff.release();
+  c->set_job.release(); c->s_inf.release(); c->item_off.release(); c->item_job.release(); c->s_aff.release();
   c->mb_fp.release(); c->mb_u64.release();
   (void)hipStreamDestroy(c->st);
   delete c;
@@ -296,6 +296,10 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, std::vector<uin
     HIPCHK(hipStreamSynchronize(c->st));
   }
   d.chunk_bound = total / 32 + n;
+  // two pairs per Miller work item only when the batch alone fills the chip
+  // (>= 65536 sets ~ 2 waves per SIMD at 1 pair per lane); below that the
+  // per-lane latency of a longer item dominates
+  d.pairs_per_item = n >= 65536 ? 2 : 1;
   if (b->scalars && !b->on_device) {
     if (int r = stage_in(c, c->scalars, b->scalars, (size_t)n, d.scalars)) return r;
   } else if (b->scalars) {
@@ -319,7 +323,7 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
   if ((r = c->sig_aff.ensure(ns)) || (r = c->h_aff.ensure(ns)) || (r = c->sig_inf.ensure(ns)) ||
       (r = c->sig_code.ensure(ns)) || (r = c->pk_code.ensure(ns)) || (r = c->rpk_aff.ensure(ns)) ||
       (r = c->rsig.ensure(ns)) || (r = c->f_set.ensure(ns + nj)) || (r = c->set_code.ensure(ns)) ||
-      (r = c->set_job.ensure(ns)) || (r = c->f_job.ensure(nj)) || (r = c->f_batch.ensure(nj)) ||
+      (r = c->set_job.ensure(ns)) || (r = c->item_off.ensure(nj + 1)) || (r = c->item_job.ensure(ns + nj + 1)) || (r = c->f_job.ensure(nj)) || (r = c->f_batch.ensure(nj)) ||
       (r = c->s_aff.ensure(nj)) || (r = c->s_inf.ensure(nj)) || (r = c->job_code.ensure(nj)) ||
       (r = c->job_result.ensure(nj)) || (r = c->f_part.ensure(4)) || (r = c->flags.ensure(4)))
     return r;
@@ -327,6 +331,7 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
   w.pk_code = c->pk_code.p; w.rpk_aff = c->rpk_aff.p; w.rsig = c->rsig.p; w.f_set = c->f_set.p;
   w.set_code = c->set_code.p; w.f_job = c->f_job.p; w.job_code = c->job_code.p; w.job_result = c->job_result.p;
   w.f_part = c->f_part.p; w.flags = c->flags.p;
+  w.item_off = c->item_off.p; w.item_job = c->item_job.p;
   w.set_job = c->set_job.p; w.f_batch = c->f_batch.p; w.s_aff = c->s_aff.p; w.s_inf = c->s_inf.p;
   return 0;
 }

@@ -17,6 +17,7 @@ struct dev_batch {
   uint32_t n_sets, n_jobs, n_raw, table_n;
   uint32_t span_log2;    // per-job reduction tree covers 2^span_log2 sets
   uint32_t chunk_bound;  // upper bound of pubkey chunks (grid of k_pk_chunk)
+  uint32_t pairs_per_item;  // Miller pairs sharing one accumulator (1, or 2 for batches that fill the GPU)
   const uint32_t* job_off;
   const uint32_t* pk_off;
   const uint32_t* pk_idx;
@@ -41,6 +42,8 @@ struct dev_work {
   int32_t* pk_code;
   g2j* rsig;          // [r_i] sigma_i
   uint32_t* set_job;  // job id of every set
+  uint32_t* item_off; // [n_jobs + 1] scan of Miller work items per job (2 sets each)
+  uint32_t* item_job; // job of every Miller work item
   g2a* s_aff;         // per job: sum [r_i] sigma_i, affine
   uint32_t* s_inf;
   fp12_t* f_set;      // per pair Miller value: n_sets set pairs, then n_jobs (-G1, S_job) pairs

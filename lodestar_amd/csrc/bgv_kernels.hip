@@ -146,13 +146,13 @@ __global__ void BGV_BULK k_chunk_count(dev_batch b, dev_work w) {
   w.chunk_off[i] = (k + PK_CHUNK - 1) / PK_CHUNK;
 }
 
-// exclusive scan of chunk_off[0..n) in place, total at [n]; one workgroup
-__global__ void __launch_bounds__(1024) k_chunk_scan(dev_batch b, dev_work w) {
+// exclusive scan of a[0..n) in place, total at a[n]; one workgroup
+__global__ void __launch_bounds__(1024) k_scan(uint32_t* a, uint32_t n) {
   __shared__ uint32_t part[1024];
-  const uint32_t t = threadIdx.x, n = b.n_sets;
+  const uint32_t t = threadIdx.x;
   const uint32_t per = (n + 1023) / 1024, beg = t * per, end = min(n, beg + per);
   uint32_t s = 0;
-  for (uint32_t i = beg; i < end; i++) s += w.chunk_off[i];
+  for (uint32_t i = beg; i < end; i++) s += a[i];
   part[t] = s;
   __syncthreads();
   for (uint32_t d = 1; d < 1024; d *= 2) {
@@ -163,11 +163,11 @@ __global__ void __launch_bounds__(1024) k_chunk_scan(dev_batch b, dev_work w) {
   }
   uint32_t run = part[t] - s;  // exclusive prefix of this thread's segment
   for (uint32_t i = beg; i < end; i++) {
-    const uint32_t c = w.chunk_off[i];
-    w.chunk_off[i] = run;
+    const uint32_t c = a[i];
+    a[i] = run;
     run += c;
   }
-  if (t == 1023) w.chunk_off[n] = part[1023];
+  if (t == 1023) a[n] = part[1023];
 }
 
 __global__ void BGV_BULK k_chunk_set(dev_batch b, dev_work w) {
@@ -294,24 +294,50 @@ __global__ void BGV_BULK k_job_s(dev_batch b, dev_work w, uint32_t span) {
 }
 
 // --------------------------------------------------------------- k_miller
-// One launch over n_sets + n_jobs pairs: (r_i PK_i, H(m_i)) for every set,
-// then (-G1, S_job) for every job.
+// Work items: every job's sets taken two at a time (one shared Fp12
+// accumulator and squaring per two pairs, miller_loop2), then one item per
+// job for its (-G1, S_job) pair.  Item offsets per job come from a scan.
+__global__ void BGV_BULK k_item_count(dev_batch b, dev_work w) {
+  const uint32_t j = gtid();
+  if (j >= b.n_jobs) return;
+  w.item_off[j] = (b.job_off[j + 1] - b.job_off[j] + b.pairs_per_item - 1) / b.pairs_per_item;
+}
+
+__global__ void BGV_BULK k_item_job(dev_batch b, dev_work w) {
+  const uint32_t j = gtid();
+  if (j >= b.n_jobs) return;
+  for (uint32_t t = w.item_off[j]; t < w.item_off[j + 1]; t++) w.item_job[t] = j;
+}
+
 __global__ void BGV_BULK k_miller(dev_batch b, dev_work w) {
   const uint32_t t = gtid();
-  if (t >= b.n_sets + b.n_jobs) return;
+  const uint32_t n_items = w.item_off[b.n_jobs];
+  if (t >= n_items + b.n_jobs) return;
   fp12_t f;
-  if (t < b.n_sets) {
-    if (w.sig_code[t] != C_OK || w.pk_code[t] != C_OK) fp12_one(f);
-    else miller_loop(f, w.rpk_aff[t], false, w.h_aff[t], false);
+  if (t < n_items) {
+    const uint32_t j = w.item_job[t];
+    const uint32_t i1 = b.job_off[j] + b.pairs_per_item * (t - w.item_off[j]);
+    const bool two = b.pairs_per_item == 2 && i1 + 1 < b.job_off[j + 1];
+    const bool ok1 = w.sig_code[i1] == C_OK && w.pk_code[i1] == C_OK;
+    const bool ok2 = !two || (w.sig_code[i1 + 1] == C_OK && w.pk_code[i1 + 1] == C_OK);
+    // a parse error rejects the whole job, so its Miller values are never used
+    if (!ok1 || !ok2) fp12_one(f);
+    else if (two) miller_loop2(f, w.rpk_aff[i1], w.h_aff[i1], w.rpk_aff[i1 + 1], w.h_aff[i1 + 1]);
+    else miller_loop(f, w.rpk_aff[i1], false, w.h_aff[i1], false);
+    w.f_set[i1] = f;
+    if (two) {
+      fp12_one(f);
+      w.f_set[i1 + 1] = f;
+    }
   } else {
-    const uint32_t j = t - b.n_sets;
+    const uint32_t j = t - n_items;
     g1a ng;
     ng.x = G1_X_MONT;
     ng.y = G1_NEG_Y_MONT;
     if (w.job_code[j] != C_OK || w.s_inf[j]) fp12_one(f);
     else miller_loop(f, ng, false, w.s_aff[j], false);
+    w.f_set[b.n_sets + j] = f;
   }
-  w.f_set[t] = f;
 }
 
 // ------------------------------------------------------ per-job f tree
@@ -584,7 +610,7 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
     case ST_HASH: BGV_LAUNCH(k_hash, b.n_sets, b, w); break;
     case ST_PK:
       BGV_LAUNCH(k_chunk_count, b.n_sets, b, w);
-      if (b.n_sets) hipLaunchKernelGGL(k_chunk_scan, dim3(1), dim3(1024), 0, st, b, w);
+      if (b.n_sets) hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, w.chunk_off, b.n_sets);
       BGV_LAUNCH(k_chunk_set, b.n_sets, b, w);
       BGV_LAUNCH(k_pk_chunk, b.chunk_bound, b, w);
       BGV_LAUNCH(k_pk, b.n_sets, b, w);
@@ -595,7 +621,12 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       for (uint32_t s = 1; s < span; s *= 2) BGV_LAUNCH(k_s_level, b.n_sets, b, w, s);
       BGV_LAUNCH(k_job_s, b.n_jobs, b, w, span);
       break;
-    case ST_MILLER: BGV_LAUNCH(k_miller, b.n_sets + b.n_jobs, b, w); break;
+    case ST_MILLER:
+      BGV_LAUNCH(k_item_count, b.n_jobs, b, w);
+      if (b.n_jobs) hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, w.item_off, b.n_jobs);
+      BGV_LAUNCH(k_item_job, b.n_jobs, b, w);
+      BGV_LAUNCH(k_miller, b.n_sets / b.pairs_per_item + 2 * b.n_jobs, b, w);  // >= items + jobs
+      break;
     case ST_F_TREE:
       for (uint32_t s = 1; s < span; s *= 2) BGV_LAUNCH(k_f_level, b.n_sets, b, w, s);
       BGV_LAUNCH(k_job_f, b.n_jobs, b, w, span);

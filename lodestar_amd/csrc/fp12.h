@@ -8,6 +8,15 @@
 
 namespace bgv {
 
+#ifndef BGV_FP6_INLINE_FP2
+#define BGV_FP6_INLINE_FP2 0
+#endif
+#if BGV_FP6_INLINE_FP2
+#define F6_MUL fp2_mul_inl
+#else
+#define F6_MUL fp2_mul
+#endif
+
 // ---------------------------------------------------------------- Fp6
 BGV_HD void fp6_zero(fp6_t& r) { r.c0 = fp2_zero(); r.c1 = fp2_zero(); r.c2 = fp2_zero(); }
 BGV_HD void fp6_one(fp6_t& r) { r.c0 = fp2_one(); r.c1 = fp2_zero(); r.c2 = fp2_zero(); }
@@ -32,13 +41,13 @@ BGV_HD void fp6_mul_v(fp6_t& r, const fp6_t& a) {
 // Karatsuba-style, 6 Fp2 products
 BGV_NI void fp6_mul(fp6_t& r, const fp6_t& a, const fp6_t& b) {
   fp2_t t0, t1, t2, s0, s1, u;
-  fp2_mul(t0, a.c0, b.c0);
-  fp2_mul(t1, a.c1, b.c1);
-  fp2_mul(t2, a.c2, b.c2);
+  F6_MUL(t0, a.c0, b.c0);
+  F6_MUL(t1, a.c1, b.c1);
+  F6_MUL(t2, a.c2, b.c2);
   // c0 = t0 + xi((a1+a2)(b1+b2) - t1 - t2)
   fp2_add(s0, a.c1, a.c2);
   fp2_add(s1, b.c1, b.c2);
-  fp2_mul(u, s0, s1);
+  F6_MUL(u, s0, s1);
   fp2_sub(u, u, t1);
   fp2_sub(u, u, t2);
   fp2_mul_xi(u, u);
@@ -47,7 +56,7 @@ BGV_NI void fp6_mul(fp6_t& r, const fp6_t& a, const fp6_t& b) {
   // c1 = (a0+a1)(b0+b1) - t0 - t1 + xi t2
   fp2_add(s0, a.c0, a.c1);
   fp2_add(s1, b.c0, b.c1);
-  fp2_mul(u, s0, s1);
+  F6_MUL(u, s0, s1);
   fp2_sub(u, u, t0);
   fp2_sub(u, u, t1);
   fp2_t x2;
@@ -57,7 +66,7 @@ BGV_NI void fp6_mul(fp6_t& r, const fp6_t& a, const fp6_t& b) {
   // c2 = (a0+a2)(b0+b2) - t0 - t2 + t1
   fp2_add(s0, a.c0, a.c2);
   fp2_add(s1, b.c0, b.c2);
-  fp2_mul(u, s0, s1);
+  F6_MUL(u, s0, s1);
   fp2_sub(u, u, t0);
   fp2_sub(u, u, t2);
   fp2_add(r.c2, u, t1);
@@ -70,20 +79,20 @@ BGV_HD void fp6_sqr(fp6_t& r, const fp6_t& a) { fp6_mul(r, a, a); }
 // a * (b0 + b1 v): 5 Fp2 products
 BGV_NI void fp6_mul_01(fp6_t& r, const fp6_t& a, const fp2_t& b0, const fp2_t& b1) {
   fp2_t t0, t1, u, s0, s1, c0, c1, c2;
-  fp2_mul(t0, a.c0, b0);
-  fp2_mul(t1, a.c1, b1);
+  F6_MUL(t0, a.c0, b0);
+  F6_MUL(t1, a.c1, b1);
   // c0 = t0 + xi a2 b1
-  fp2_mul(u, a.c2, b1);
+  F6_MUL(u, a.c2, b1);
   fp2_mul_xi(u, u);
   fp2_add(c0, u, t0);
   // c1 = (a0+a1)(b0+b1) - t0 - t1
   fp2_add(s0, a.c0, a.c1);
   fp2_add(s1, b0, b1);
-  fp2_mul(u, s0, s1);
+  F6_MUL(u, s0, s1);
   fp2_sub(u, u, t0);
   fp2_sub(c1, u, t1);
   // c2 = t1 + a2 b0
-  fp2_mul(u, a.c2, b0);
+  F6_MUL(u, a.c2, b0);
   fp2_add(c2, u, t1);
   r.c0 = c0; r.c1 = c1; r.c2 = c2;
 }
@@ -91,10 +100,10 @@ BGV_NI void fp6_mul_01(fp6_t& r, const fp6_t& a, const fp2_t& b0, const fp2_t& b
 // a * (b1 v): 3 Fp2 products
 BGV_NI void fp6_mul_1(fp6_t& r, const fp6_t& a, const fp2_t& b1) {
   fp2_t c0, c1, c2;
-  fp2_mul(c0, a.c2, b1);
+  F6_MUL(c0, a.c2, b1);
   fp2_mul_xi(c0, c0);
-  fp2_mul(c1, a.c0, b1);
-  fp2_mul(c2, a.c1, b1);
+  F6_MUL(c1, a.c0, b1);
+  F6_MUL(c2, a.c1, b1);
   r.c0 = c0; r.c1 = c1; r.c2 = c2;
 }
 

@@ -110,4 +110,35 @@ BGV_NI void miller_loop(fp12_t& f, const g1a& P, bool p_inf, const g2a& Q, bool 
   fp12_conj(f, f);  // x < 0
 }
 
+// Two pairs with ONE shared accumulator: f = f_{x,Q1}(P1) * f_{x,Q2}(P2),
+// so the Fp12 squaring of every iteration is paid once for both pairs
+// (the multi-Miller loop of blst's miller_loop_n, at width 2).
+BGV_NI void miller_loop2(fp12_t& f, const g1a& P1, const g2a& Q1, const g1a& P2, const g2a& Q2) {
+  g2p_t T1, T2;
+  T1.x = Q1.x; T1.y = Q1.y; T1.z = fp2_one();
+  T2.x = Q2.x; T2.y = Q2.y; T2.z = fp2_one();
+  fp2_t a0, a1, b1;
+  fp12_one(f);
+  for (int b = 62; b >= 0; b--) {
+    if (b != 62) fp12_sqr(f, f);
+    miller_dbl_step(T1, a0, a1, b1, P1.x, P1.y);
+    if (b == 62) {  // f = 1 * line
+      f.c0.c0 = a0;
+      f.c0.c1 = a1;
+      f.c1.c1 = b1;
+    } else {
+      fp12_mul_line(f, f, a0, a1, b1);
+    }
+    miller_dbl_step(T2, a0, a1, b1, P2.x, P2.y);
+    fp12_mul_line(f, f, a0, a1, b1);
+    if ((BLS_X_ABS >> b) & 1ull) {
+      miller_add_step(T1, a0, a1, b1, Q1, P1.x, P1.y);
+      fp12_mul_line(f, f, a0, a1, b1);
+      miller_add_step(T2, a0, a1, b1, Q2, P2.x, P2.y);
+      fp12_mul_line(f, f, a0, a1, b1);
+    }
+  }
+  fp12_conj(f, f);  // x < 0
+}
+
 }  // namespace bgv

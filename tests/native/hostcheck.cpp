@@ -90,6 +90,10 @@ int hc_hash_to_g2(const uint8_t* msg32, uint8_t* out192) { g2j r; hash_to_g2(r, 
 void hc_miller_loop(const uint8_t* p96, const uint8_t* q192, uint8_t* out576) {
   g1a p; g2a q; get_g1a(p, p96); get_g2a(q, q192); fp12_t f; miller_loop(f, p, false, q, false); put_fp12(out576, f);
 }
+void hc_miller_loop2(const uint8_t* p1, const uint8_t* q1, const uint8_t* p2, const uint8_t* q2, uint8_t* out576) {
+  g1a P1, P2; g2a Q1, Q2; get_g1a(P1, p1); get_g2a(Q1, q1); get_g1a(P2, p2); get_g2a(Q2, q2);
+  fp12_t f; miller_loop2(f, P1, Q1, P2, Q2); put_fp12(out576, f);
+}
 void hc_miller_dbl_step(const uint8_t* t288, const uint8_t* p96, uint8_t* t_out288, uint8_t* line288) {
   g2p_t T; get_fp2(T.x, t288); get_fp2(T.y, t288 + 96); get_fp2(T.z, t288 + 192);
   g1a p; get_g1a(p, p96); fp2_t a0, a1, b1;

@@ -235,3 +235,16 @@ def test_miller_steps_and_pairing():
     got = B.tower_to_f12(H.b_tower(fe.raw))
     want = B.pairing(P, Q)
     assert B.f12_eq(got, B.f12_pow(want, 3))
+
+
+def test_miller_loop2_equals_product_of_single_loops():
+    """the 2-pair shared-accumulator loop used by k_miller is bit-identical to
+    the product of two single Miller loops (same tower element, no FE)"""
+    P1, Q1 = B.E1.mul(B.G1, 5), B.E2.mul(B.G2, 9)
+    P2, Q2 = B.E1.mul(B.G1, 123), B.E2.mul(B.G2, 77)
+    o1, o2, o12, prod = H.buf(576), H.buf(576), H.buf(576), H.buf(576)
+    lib.hc_miller_loop(H.g1_b(P1), H.g2_b(Q1), o1)
+    lib.hc_miller_loop(H.g1_b(P2), H.g2_b(Q2), o2)
+    lib.hc_fp12_mul(o1.raw, o2.raw, prod)
+    lib.hc_miller_loop2(H.g1_b(P1), H.g2_b(Q1), H.g1_b(P2), H.g2_b(Q2), o12)
+    assert o12.raw == prod.raw
