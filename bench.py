@@ -101,6 +101,23 @@ def fpmul_counts():
     return json.load(open(p)) if os.path.exists(p) else None
 
 
+STAGE_KERNEL = {"sig_decode_subgroup": "k_sig", "hash_to_g2": "k_hash", "pk_aggregate_scale": "k_pk_chunk",
+                "sig_scale": "k_sig_scale", "miller_loop": "k_miller"}
+
+
+def pmc_traffic(stage: str):
+    """HBM-side bytes per launch of the stage's main kernel from the committed
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.json)."""
+    p = os.path.join(ROOT, "tools", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None, None
+    t = json.load(open(p))
+    k = t["kernels"].get(STAGE_KERNEL.get(stage, ""), None)
+    if not k:
+        return None, None
+    return k["fetch_bytes"] + k["write_bytes"], t["source"]
+
+
 def cpu_baseline(budget_s: float = 10.0):
     """oracle C restatement (oracle/libbls_ref.so) timed on this host's cores
     on a bounded sample of the same workload; None when not built."""
@@ -223,10 +240,15 @@ def main():
             per_set = counts["per_set"][dom]
             shard_sets = arrays["n_sets"]
             achieved = per_set * shard_sets / (stage_ms[dom] * 1e-3) / 1e9
+            traffic, tsrc = pmc_traffic(dom)
             roof = {"bound": "valu-int32", "kernel": dom, "achieved": round(achieved, 3), "peak": round(peak_fpmul, 3),
-                    "unit": "G Fp-mul/s", "frac": round(achieved / peak_fpmul, 4), "traffic": None,
-                    "per_set_fpmul": per_set, "kernel_ms": round(stage_ms[dom], 3),
-                    "mad_u64_lane_ops_per_s": mad_rate, "fpmul_microbench_G_per_s": round(fpm_rate, 3)}
+                    "unit": "G Fp-mul/s", "frac": round(achieved / peak_fpmul, 4), "traffic": traffic,
+                    "traffic_unit": "bytes per launch (FETCH_SIZE + WRITE_SIZE, raw)", "traffic_source": tsrc,
+                    "algorithmic_bytes_per_launch": shard_sets * (96 + 192 + 576),
+                    "per_set_fpmul": per_set, "sets_per_launch": shard_sets, "kernel_ms": round(stage_ms[dom], 3),
+                    "peak_def": "measured v_mad_u64_u32 lane-ops/s / 288 (12x32-bit CIOS product count)",
+                    "mad_u64_lane_ops_per_s": mad_rate, "peak_fpmul28_G_per_s": round(mad_rate / 393 / 1e9, 3),
+                    "fpmul_microbench_G_per_s": round(fpm_rate, 3)}
         else:
             roof = {"bound": "valu-int32", "kernel": dom, "achieved": None, "peak": round(peak_fpmul, 3),
                     "unit": "G Fp-mul/s", "frac": None, "traffic": None,
