@@ -11,6 +11,7 @@
 #include <string.h>
 #include <stdio.h>
 #include <stdarg.h>
+#include <stdlib.h>
 #include <vector>
 #include <string>
 
@@ -61,6 +62,7 @@ struct dbuf {
 
 struct bgv_ctx {
   int device = 0;
+  int miller_mode = -1;  // BGV_MILLER=serial|coop forces one Miller kernel (A/B tests); -1 = by batch size
   hipStream_t st = nullptr;
   hipEvent_t ev[ST_COUNT + 1] = {};
   // index2pubkey table (grown by copy) and synthetic secret keys
@@ -126,6 +128,7 @@ int bgv_open(int device, bgv_ctx** out) {
   HIPCHK(hipSetDevice(device));
   bgv_ctx* c = new bgv_ctx();
   c->device = device;
+  if (const char* m = getenv("BGV_MILLER")) c->miller_mode = strcmp(m, "serial") != 0 ? 1 : 0;
   HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
   for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
   *out = c;
@@ -300,6 +303,9 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, std::vector<uin
   // (>= 65536 sets ~ 2 waves per SIMD at 1 pair per lane); below that the
   // per-lane latency of a longer item dominates
   d.pairs_per_item = n >= 65536 ? 2 : 1;
+  // six-lane cooperative Miller loop (low latency) unless the batch alone
+  // fills the GPU, where the one-lane loop does less work per pair
+  d.miller_coop = c->miller_mode >= 0 ? (uint32_t)c->miller_mode : (n < 65536 ? 1u : 0u);
   if (b->scalars && !b->on_device) {
     if (int r = stage_in(c, c->scalars, b->scalars, (size_t)n, d.scalars)) return r;
   } else if (b->scalars) {

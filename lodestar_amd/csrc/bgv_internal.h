@@ -17,6 +17,7 @@ struct dev_batch {
   uint32_t n_sets, n_jobs, n_raw, table_n;
   uint32_t span_log2;    // per-job reduction tree covers 2^span_log2 sets
   uint32_t chunk_bound;  // upper bound of pubkey chunks (grid of k_pk_chunk)
+  uint32_t miller_coop;     // 1: six-lane cooperative Miller loop (miller_coop.h)
   uint32_t pairs_per_item;  // Miller pairs sharing one accumulator (1, or 2 for batches that fill the GPU)
   const uint32_t* job_off;
   const uint32_t* pk_off;

@@ -22,6 +22,7 @@
 //                 (the worker's per-job retry, multithread/worker.ts:74-85)
 #include "bgv_internal.h"
 #include "fp12_wave.h"
+#include "miller_coop.h"
 
 namespace bgv {
 
@@ -340,6 +341,53 @@ __global__ void BGV_BULK k_miller(dev_batch b, dev_work w) {
   }
 }
 
+// Cooperative variant (miller_coop.h): 10 pairs per 64-lane workgroup, six
+// lanes per pair, pair t < n_sets is (r_t PK_t, H(m_t)), then (-G1, S_job).
+__global__ void __launch_bounds__(64, BGV_WAVES) k_miller_coop(dev_batch b, dev_work w) {
+  __shared__ coop_grp sm[COOP_GROUPS];
+  const uint32_t lane = threadIdx.x, grp = lane / COOP_LANES, k = lane % COOP_LANES;
+  const uint32_t t = blockIdx.x * COOP_GROUPS + grp;
+  const uint32_t n_pairs = b.n_sets + b.n_jobs;
+  const bool in_range = grp < COOP_GROUPS && t < n_pairs;
+  bool active = in_range;
+  if (in_range) {
+    g1a P;
+    g2a Q;
+    if (t < b.n_sets) {
+      active = w.sig_code[t] == C_OK && w.pk_code[t] == C_OK;
+      P = w.rpk_aff[t];
+      Q = w.h_aff[t];
+    } else {
+      const uint32_t j = t - b.n_sets;
+      active = w.job_code[j] == C_OK && !w.s_inf[j];
+      P.x = G1_X_MONT;
+      P.y = G1_NEG_Y_MONT;
+      Q = w.s_aff[j];
+    }
+    if (active && k == 0) {
+      coop_grp& g = sm[grp];
+      g.T[0] = Q.x;
+      g.T[1] = Q.y;
+      g.T[2] = fp2_one();
+      g.Q[0] = Q.x;
+      g.Q[1] = Q.y;
+      g.px.c0 = P.x;
+      fp_set_zero(g.px.c1);
+      g.py.c0 = P.y;
+      fp_set_zero(g.py.c1);
+    }
+  }
+  __syncthreads();
+  coop_miller(sm[grp < COOP_GROUPS ? grp : 0], k, active);
+  if (in_range) {
+    fp2_t v;
+    if (active) v = sm[grp].f[k];
+    else v = k == 0 ? fp2_one() : fp2_zero();  // skipped pair contributes 1
+    fp2_t* dst = reinterpret_cast<fp2_t*>(&w.f_set[t]) + (k & 1) * 3 + (k >> 1);
+    *dst = v;
+  }
+}
+
 // ------------------------------------------------------ per-job f tree
 __global__ void BGV_BULK k_f_level(dev_batch b, dev_work w, uint32_t s) {
   const uint32_t i = gtid();
@@ -622,6 +670,11 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       BGV_LAUNCH(k_job_s, b.n_jobs, b, w, span);
       break;
     case ST_MILLER:
+      if (b.miller_coop) {
+        const uint32_t pairs = b.n_sets + b.n_jobs;
+        if (pairs) hipLaunchKernelGGL(k_miller_coop, dim3((pairs + COOP_GROUPS - 1) / COOP_GROUPS), dim3(64), 0, st, b, w);
+        break;
+      }
       BGV_LAUNCH(k_item_count, b.n_jobs, b, w);
       if (b.n_jobs) hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, w.item_off, b.n_jobs);
       BGV_LAUNCH(k_item_job, b.n_jobs, b, w);
