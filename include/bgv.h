@@ -111,8 +111,9 @@ typedef struct bgv_batch {
   uint32_t on_device;
 } bgv_batch;
 
-/* Timings of the last bgv_verify call (ms, HIP events on the context's
- * stream) plus the counters the reference pool exports as
+/* Timings of the last bgv_verify call (ms, HIP events around each stage on
+ * the stream it ran on; stages 0-3 run concurrently on three streams, so their
+ * times overlap and total_ms is less than their sum) plus the counters the reference pool exports as
  * lodestar_bls_thread_pool_* metrics (metrics/metrics/lodestar.ts:350-430). */
 #define BGV_N_STAGES 12
 typedef struct bgv_stats {

@@ -63,8 +63,11 @@ struct dbuf {
 struct bgv_ctx {
   int device = 0;
   int miller_mode = -1;  // BGV_MILLER=serial|coop forces one Miller kernel (A/B tests); -1 = by batch size
-  hipStream_t st = nullptr;
-  hipEvent_t ev[ST_COUNT + 1] = {};
+  bool overlap = true;    // BGV_OVERLAP=0 runs every stage on one stream (A/B tests)
+  hipStream_t st = nullptr, st_hash = nullptr, st_pk = nullptr;
+  hipEvent_t ev[ST_COUNT + 1] = {};   // ev[s] = start of stage s on its stream
+  hipEvent_t ev_end[ST_COUNT] = {};   // end of stage s on its stream
+  hipEvent_t ev_fork = nullptr;
   // index2pubkey table (grown by copy) and synthetic secret keys
   g1a* table = nullptr;
   uint32_t table_n = 0, table_cap = 0;
@@ -129,8 +132,13 @@ int bgv_open(int device, bgv_ctx** out) {
   bgv_ctx* c = new bgv_ctx();
   c->device = device;
   if (const char* m = getenv("BGV_MILLER")) c->miller_mode = strcmp(m, "serial") != 0 ? 1 : 0;
+  if (const char* o = getenv("BGV_OVERLAP")) c->overlap = strcmp(o, "0") != 0;
   HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&c->st_hash, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&c->st_pk, hipStreamNonBlocking));
   for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+  for (auto& e : c->ev_end) HIPCHK(hipEventCreate(&e));
+  HIPCHK(hipEventCreate(&c->ev_fork));
   *out = c;
   return BGV_OK;
 }
@@ -139,7 +147,11 @@ int bgv_close(bgv_ctx* c) {
   if (!c) return BGV_OK;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->st);
+  (void)hipStreamSynchronize(c->st_hash);
+  (void)hipStreamSynchronize(c->st_pk);
   for (auto& e : c->ev) (void)hipEventDestroy(e);
+  for (auto& e : c->ev_end) (void)hipEventDestroy(e);
+  (void)hipEventDestroy(c->ev_fork);
   if (c->table) (void)hipFree(c->table);
   c->sk.release();
   c->job_off.release(); c->pk_off.release(); c->pk_idx.release(); c->sig_len.release();
@@ -151,6 +163,8 @@ int bgv_close(bgv_ctx* c) {
   c->set_job.release(); c->s_inf.release(); c->item_off.release(); c->item_job.release(); c->s_aff.release();
   c->mb_fp.release(); c->mb_u64.release();
   (void)hipStreamDestroy(c->st);
+  (void)hipStreamDestroy(c->st_hash);
+  (void)hipStreamDestroy(c->st_pk);
   delete c;
   return BGV_OK;
 }
@@ -343,11 +357,30 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
 }
 
 // run stages [from, to) with an event before each
+// The three input stages are independent: signature decode (+ its scaling),
+// hash_to_G2 and pubkey aggregation read disjoint inputs and write disjoint
+// buffers (bgv_kernels.hip), so they run on three streams and join before the
+// signature tree.  Each on its own leaves SIMDs idle (1.5 waves per SIMD at C4,
+// ~60% VALU busy); together they fill the gaps.
 static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int from, int to) {
+  const bool fork = c->overlap && from <= ST_SIG && to > ST_S_TREE;
+  if (fork) {
+    HIPCHK(hipEventRecord(c->ev_fork, c->st));
+    HIPCHK(hipStreamWaitEvent(c->st_hash, c->ev_fork, 0));
+    HIPCHK(hipStreamWaitEvent(c->st_pk, c->ev_fork, 0));
+  }
   for (int s = from; s < to; s++) {
-    HIPCHK(hipEventRecord(c->ev[s], c->st));
-    launch_stage(c->st, s, d, w);
+    hipStream_t st = c->st;
+    if (fork && s == ST_HASH) st = c->st_hash;
+    if (fork && s == ST_PK) st = c->st_pk;
+    if (fork && s == ST_S_TREE) {
+      HIPCHK(hipStreamWaitEvent(c->st, c->ev_end[ST_HASH], 0));
+      HIPCHK(hipStreamWaitEvent(c->st, c->ev_end[ST_PK], 0));
+    }
+    HIPCHK(hipEventRecord(c->ev[s], st));
+    launch_stage(st, s, d, w);
     HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev_end[s], st));
   }
   HIPCHK(hipEventRecord(c->ev[to], c->st));
   return 0;
@@ -369,7 +402,7 @@ int bgv_verify(bgv_ctx* c, const bgv_batch* b, int32_t* job_result, int32_t* set
   HIPCHK(hipStreamSynchronize(c->st));
   if (stats) {
     memset(stats, 0, sizeof *stats);
-    for (int s = 0; s < ST_COUNT && s < BGV_N_STAGES; s++) HIPCHK(hipEventElapsedTime(&stats->stage_ms[s], c->ev[s], c->ev[s + 1]));
+    for (int s = 0; s < ST_COUNT && s < BGV_N_STAGES; s++) HIPCHK(hipEventElapsedTime(&stats->stage_ms[s], c->ev[s], c->ev_end[s]));
     HIPCHK(hipEventElapsedTime(&stats->total_ms, c->ev[0], c->ev[ST_COUNT]));
     stats->n_sets = d.n_sets;
     stats->n_jobs = d.n_jobs;

@@ -246,6 +246,8 @@ w("// hash_to_field: 64-byte big-endian e = hi 2^256 + lo ; mont(e) = mont_mul(h
 w("BGV_CONST fp_t H2F_K = " + fp_lit((1 << 256) * RM * RM % P, False) + ";")
 w("// 1/2 in Montgomery form (Fp2 sqrt)")
 w("BGV_CONST fp_t FP_HALF = " + fp_lit(pow(2, -1, P)) + ";")
+w("// R^3 mod p (plain): Montgomery fix-up after a binary-GCD inverse of a Montgomery value")
+w("BGV_CONST fp_t R3_MOD = " + fp_lit(RM ** 3 % P, False) + ";")
 w("")
 w("}  // namespace bgv")
 
