@@ -109,6 +109,26 @@ BGV_HD bool fp2_lex_largest(const fp2_t& a) {
 //   t = (a0 + d) / 2,  s = t^((p-3)/4)
 //   s^2 t == 1 :  x = s t + (a1 s / 2) i
 //   otherwise  :  x = (a1 s / 2) - (s t) i      (then -t is the square)
+// fp2_sqrt_tail is the second half, for a1 != 0 and a known root d of the
+// norm (either sign works: the two choices of t differ by a non-square factor).
+BGV_NI void fp2_sqrt_tail(fp2_t& r, const fp2_t& a, const fp_t& d) {
+  fp_t t, s, st, s2t, as;
+  fp_add(t, a.c0, d);
+  fp_half(t, t);
+  fp_pow(s, t, EXP_P_MINUS_3_DIV_4);
+  fp_mul(st, s, t);
+  fp_mul(s2t, st, s);
+  fp_mul(as, a.c1, s);
+  fp_half(as, as);
+  if (fp_eq(s2t, FP_ONE)) {
+    r.c0 = st;
+    r.c1 = as;
+  } else {
+    r.c0 = as;
+    fp_neg(r.c1, st);
+  }
+}
+
 // a1 == 0 is handled directly in Fp.  Returns false iff a is a non-square.
 BGV_NI bool fp2_sqrt(fp2_t& r, const fp2_t& a) {
   if (fp_is_zero(a.c1)) {
@@ -129,21 +149,7 @@ BGV_NI bool fp2_sqrt(fp2_t& r, const fp2_t& a) {
   fp_t n, d;
   fp2_norm(n, a);
   if (!fp_sqrt(d, n)) return false;
-  fp_t t, s, st, s2t, as;
-  fp_add(t, a.c0, d);
-  fp_half(t, t);
-  fp_pow(s, t, EXP_P_MINUS_3_DIV_4);
-  fp_mul(st, s, t);
-  fp_mul(s2t, st, s);
-  fp_mul(as, a.c1, s);
-  fp_half(as, as);
-  if (fp_eq(s2t, FP_ONE)) {
-    r.c0 = st;
-    r.c1 = as;
-  } else {
-    r.c0 = as;
-    fp_neg(r.c1, st);
-  }
+  fp2_sqrt_tail(r, a, d);
   return true;
 }
 

@@ -169,11 +169,29 @@ BGV_NI void map_to_curve_sswu(g2a& out, const fp2_t& u) {
   fp2_add(t, t, SSWU_A);
   fp2_mul(gx2, t, x2);
   fp2_add(gx2, gx2, SSWU_B);
-  const bool sq = fp2_is_square(gx1);
+  // gx1 is a square in Fp2 iff norm(gx1) is one in Fp, and the root of the
+  // norm is the first half of fp2_sqrt anyway: one exponentiation answers the
+  // test and starts the root.  Otherwise d^2 = -norm(gx1) and, as
+  // gx2 = Z^3 u^6 gx1, sqrt(norm(gx2)) = sqrt(-norm(Z)^3) norm(u)^3 d.
+  // (RFC 9380 6.6.2 computes is_square(gx1) and sqrt() separately: 4 exponentiations.)
+  fp_t n1, d, chk, nu, nu3, d2;
+  fp2_norm(n1, gx1);
+  fp_pow(d, n1, EXP_P_PLUS_1_DIV_4);
+  fp_sqr(chk, d);
+  const bool sq = fp_eq(chk, n1);
+  fp2_norm(nu, u);
+  fp_sqr(nu3, nu);
+  fp_mul(nu3, nu3, nu);
+  fp_mul(d2, d, nu3);
+  fp_mul(d2, d2, SSWU_SQRT_NEG_NZ3);
   fp2_t x, g, y;
   fp2_select(x, sq, x1, x2);
   fp2_select(g, sq, gx1, gx2);
-  fp2_sqrt(y, g);
+  if (!sq) d = d2;
+  // exceptional u (den == 0: x1 = B/(ZA), the gx2 identity does not hold) and
+  // g with a zero imaginary part take the general root
+  if (fp_is_zero(g.c1) || (!sq && fp2_is_zero(den))) fp2_sqrt(y, g);
+  else fp2_sqrt_tail(y, g, d);
   if (fp2_sgn0(u) != fp2_sgn0(y)) fp2_neg(y, y);
   out.x = x;
   out.y = y;

@@ -37,10 +37,16 @@ def test_fp_ops():
         assert H.b_fp(o.raw) == (a + b) % B.P
         lib.hc_fp_sub(H.fp_b(a), H.fp_b(b), o)
         assert H.b_fp(o.raw) == (a - b) % B.P
-    for a in [1, 2, B.P - 1, rfp()]:
+    # divstep inversion: edge values (Montgomery images 1, 2, p-1 included) and random values
+    rinv = pow(2**384, -1, B.P)
+    edge = [1, 2, 3, B.P - 1, B.P - 2, (B.P - 1) // 2, rinv, 2 * rinv % B.P, (B.P - 1) * rinv % B.P, 2**380 % B.P]
+    for a in edge + [rfp() for _ in range(400)]:
         o = H.buf(48)
         lib.hc_fp_inv(H.fp_b(a), o)
-        assert H.b_fp(o.raw) * a % B.P == 1
+        assert H.b_fp(o.raw) * a % B.P == 1, hex(a)
+    o = H.buf(48)
+    lib.hc_fp_inv(H.fp_b(0), o)
+    assert H.b_fp(o.raw) == 0
     # edge values
     for a, b in [(B.P - 1, B.P - 1), (0, B.P - 1), (1, 1)]:
         o = H.buf(48)
@@ -198,7 +204,7 @@ def test_hash_to_g2_stages():
     lib.hc_hash_to_field(msg, o)
     u0, u1 = B.hash_to_field_fp2(msg, 2, B.DST_POP)
     assert H.b_fp2(o.raw[:96]) == u0 and H.b_fp2(o.raw[96:]) == u1
-    for u in (u0, u1, rfp2()):
+    for u in [u0, u1, B.F2_ZERO, (1, 0)] + [rfp2() for _ in range(12)]:
         lib.hc_sswu(H.fp2_b(u), o)
         q = B.map_to_curve_sswu(u)
         assert B.E2.eq(H.b_g2(o.raw), q)

@@ -236,6 +236,12 @@ w("BGV_CONST fp2_t SSWU_B = " + fp2_lit(Bc) + ";")
 w("BGV_CONST fp2_t SSWU_Z = " + fp2_lit(Z) + ";")
 w("BGV_CONST fp2_t SSWU_MINUS_B_OVER_A = " + fp2_lit(f2_mul(f2_neg(Bc), f2_inv(A))) + ";")
 w("BGV_CONST fp2_t SSWU_B_OVER_ZA = " + fp2_lit(f2_mul(Bc, f2_inv(f2_mul(Z, A)))) + ";")
+w("// sqrt(-norm(Z)^3) in Fp: gx2 = Z^3 u^6 gx1, so when norm(gx1) is a non-square with")
+w("// d = norm(gx1)^((p+1)/4) (d^2 = -norm(gx1)), sqrt(norm(gx2)) = this * norm(u)^3 * d")
+_nz3 = (-pow((Z[0] * Z[0] + Z[1] * Z[1]) % P, 3, P)) % P
+_c = pow(_nz3, (P + 1) // 4, P)
+assert _c * _c % P == _nz3
+w("BGV_CONST fp_t SSWU_SQRT_NEG_NZ3 = " + fp_lit(_c) + ";")
 w("// 3-isogeny E2' -> E2 (RFC 9380 appendix E.3), lowest degree first")
 w("BGV_CONST fp2_t ISO_XNUM[4] = {" + ", ".join(fp2_lit(c) for c in ISO_XNUM) + "};")
 w("BGV_CONST fp2_t ISO_XDEN[3] = {" + ", ".join(fp2_lit(c) for c in ISO_XDEN) + "};")
@@ -248,6 +254,9 @@ w("// 1/2 in Montgomery form (Fp2 sqrt)")
 w("BGV_CONST fp_t FP_HALF = " + fp_lit(pow(2, -1, P)) + ";")
 w("// R^3 mod p (plain): Montgomery fix-up after a binary-GCD inverse of a Montgomery value")
 w("BGV_CONST fp_t R3_MOD = " + fp_lit(RM ** 3 % P, False) + ";")
+w("// p as 13 signed 30-bit limbs and p^-1 mod 2^30 (divstep inversion, fp.h)")
+w("BGV_CONST int32_t P_S30[13] = {" + ", ".join("0x%08x" % ((P >> (30 * i)) & (2**30 - 1)) for i in range(13)) + "};")
+w("BGV_CONST uint32_t P_INV30 = 0x%08xu;" % pow(P, -1, 2**30))
 w("")
 w("}  // namespace bgv")
 
