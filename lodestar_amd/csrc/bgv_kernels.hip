@@ -32,6 +32,9 @@ namespace bgv {
 #define BGV_WAVES 2
 #endif
 #define BGV_BULK __launch_bounds__(64, BGV_WAVES)
+#ifndef BGV_MILLER_WAVES
+#define BGV_MILLER_WAVES BGV_WAVES
+#endif
 
 __device__ __forceinline__ uint32_t gtid() { return blockIdx.x * blockDim.x + threadIdx.x; }
 
@@ -310,7 +313,7 @@ __global__ void BGV_BULK k_item_job(dev_batch b, dev_work w) {
   for (uint32_t t = w.item_off[j]; t < w.item_off[j + 1]; t++) w.item_job[t] = j;
 }
 
-__global__ void BGV_BULK k_miller(dev_batch b, dev_work w) {
+__global__ void __launch_bounds__(64, BGV_MILLER_WAVES) k_miller(dev_batch b, dev_work w) {
   const uint32_t t = gtid();
   const uint32_t n_items = w.item_off[b.n_jobs];
   if (t >= n_items + b.n_jobs) return;
