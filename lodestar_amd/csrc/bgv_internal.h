@@ -77,6 +77,7 @@ void launch_table_from_compressed(hipStream_t st, const uint8_t* in, g1a* out, u
 void launch_table_from_uncompressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n);
 void launch_table_export(hipStream_t st, const g1a* tab, uint8_t* out, uint32_t n);
 void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work& w);
+void launch_fp12_tail(hipStream_t st, int stage, const dev_batch& b, const dev_work& w);  // bgv_tail.hip
 void launch_combine_final(hipStream_t st, const fp12_t* parts, uint32_t n, uint32_t* flag);
 void launch_fp12_convert(hipStream_t st, const fp12_t* in, fp12_t* out, uint32_t n, bool to_mont);
 void launch_gen_keys(hipStream_t st, g1a* table, uint32_t* sk, uint32_t first, uint32_t n, uint64_t seed);

@@ -17,11 +17,28 @@
 //   k_miller      f_i = MillerLoop([r_i] PK_i, H(m_i))
 //   k_job         per job: f_j = prod f_i * MillerLoop(-G1, sum [r_i] sigma_i),
 //                 first parse error of the job (set order)
-//   k_batch_final whole-batch product + ONE final exponentiation
-//   k_job_final   per-job final exponentiation only if the batch check failed
-//                 (the worker's per-job retry, multithread/worker.ts:74-85)
+//   (bgv_tail.hip) per-job and whole-batch Fp12 product trees, ONE final
+//                 exponentiation for the batch, per-job final exponentiation
+//                 only if the batch check failed (the worker's per-job retry,
+//                 multithread/worker.ts:74-85)
+// Code generation of this translation unit (measured on MI355X, r01):
+//  * every Fp product is a call to one non-inlined leaf with its operands in
+//    VGPRs (fp.h BGV_FPMUL_CALL) and the Fp2 layer is inlined, so Fp2
+//    temporaries live in registers instead of on the scratch stack;
+//  * the Miller kernel runs at 1 wave/SIMD: its 512-register budget takes
+//    the spills in AGPRs (k_miller 37.9 -> 33.1 ms at C4).
+// The Fp12 product trees and final exponentiations prefer the inlined
+// product and live in bgv_tail.hip.
+#ifndef BGV_FPMUL_CALL
+#define BGV_FPMUL_CALL 1
+#endif
+#ifndef BGV_FP2_INLINE
+#define BGV_FP2_INLINE 1
+#endif
+#ifndef BGV_MILLER_WAVES
+#define BGV_MILLER_WAVES 1
+#endif
 #include "bgv_internal.h"
-#include "fp12_wave.h"
 #include "miller_coop.h"
 
 namespace bgv {
@@ -150,28 +167,39 @@ __global__ void BGV_BULK k_chunk_count(dev_batch b, dev_work w) {
   w.chunk_off[i] = (k + PK_CHUNK - 1) / PK_CHUNK;
 }
 
-// exclusive scan of a[0..n) in place, total at a[n]; one workgroup
+// exclusive scan of a[0..n) in place, total at a[n]; one workgroup walking
+// 1024-element tiles with coalesced loads: wave scan by shuffles, the 16 wave
+// totals scanned by wave 0, a running carry across tiles
 __global__ void __launch_bounds__(1024) k_scan(uint32_t* a, uint32_t n) {
-  __shared__ uint32_t part[1024];
-  const uint32_t t = threadIdx.x;
-  const uint32_t per = (n + 1023) / 1024, beg = t * per, end = min(n, beg + per);
-  uint32_t s = 0;
-  for (uint32_t i = beg; i < end; i++) s += a[i];
-  part[t] = s;
-  __syncthreads();
-  for (uint32_t d = 1; d < 1024; d *= 2) {
-    const uint32_t v = t >= d ? part[t - d] : 0u;
+  __shared__ uint32_t wsum[16];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wid = t >> 6;
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < n; base += 1024u) {
+    const uint32_t i = base + t;
+    const uint32_t v = i < n ? a[i] : 0u;
+    uint32_t x = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
     __syncthreads();
-    part[t] += v;
+    if (wid == 0) {
+      uint32_t s = lane < 16 ? wsum[lane] : 0u;
+#pragma unroll
+      for (uint32_t d = 1; d < 16; d <<= 1) {
+        const uint32_t y = __shfl_up(s, d, 64);
+        if (lane >= d) s += y;
+      }
+      if (lane < 16) wsum[lane] = s;
+    }
     __syncthreads();
+    if (i < n) a[i] = carry + (wid ? wsum[wid - 1] : 0u) + x - v;
+    carry += wsum[15];
+    __syncthreads();  // wsum is rewritten by the next tile
   }
-  uint32_t run = part[t] - s;  // exclusive prefix of this thread's segment
-  for (uint32_t i = beg; i < end; i++) {
-    const uint32_t c = a[i];
-    a[i] = run;
-    run += c;
-  }
-  if (t == 1023) a[n] = part[1023];
+  if (t == 0) a[n] = carry;
 }
 
 __global__ void BGV_BULK k_chunk_set(dev_batch b, dev_work w) {
@@ -391,91 +419,12 @@ __global__ void __launch_bounds__(64, BGV_WAVES) k_miller_coop(dev_batch b, dev_
   }
 }
 
-// ------------------------------------------------------ per-job f tree
-__global__ void BGV_BULK k_f_level(dev_batch b, dev_work w, uint32_t s) {
-  const uint32_t i = gtid();
-  if (i >= b.n_sets) return;
-  const uint32_t j = w.set_job[i];
-  const uint32_t beg = b.job_off[j], end = b.job_off[j + 1];
-  if (((i - beg) % (2 * s)) != 0 || i + s >= end) return;
-  fp12_t a = w.f_set[i];
-  fp12_mul(a, a, w.f_set[i + s]);
-  w.f_set[i] = a;
-}
-
-__global__ void BGV_BULK k_job_f(dev_batch b, dev_work w, uint32_t span) {
-  const uint32_t j = gtid();
-  if (j >= b.n_jobs) return;
-  const uint32_t beg = b.job_off[j], end = b.job_off[j + 1];
-  fp12_t f;
-  if (w.job_code[j] != C_OK) {
-    fp12_one(f);  // rejected jobs take no part in the batch product
-  } else {
-    f = w.f_set[beg];
-    for (uint32_t i = beg + span; i < end; i += span) fp12_mul(f, f, w.f_set[i]);
-    fp12_mul(f, f, w.f_set[b.n_sets + j]);
-  }
-  w.f_job[j] = f;
-  w.f_batch[j] = f;
-}
-
-// ---------------------------------------------------------- batch product
-__global__ void BGV_BULK k_batch_level(dev_batch b, dev_work w, uint32_t s) {
-  const uint32_t j = gtid();
-  if (j >= b.n_jobs || (j % (2 * s)) != 0 || j + s >= b.n_jobs) return;
-  fp12_t a = w.f_batch[j];
-  fp12_mul(a, a, w.f_batch[j + s]);
-  w.f_batch[j] = a;
-}
-
-// the whole-batch check: ONE final exponentiation, wave-cooperative (fp12_wave.h)
-__global__ void BGV_BULK k_batch_final(dev_batch b, dev_work w) {
-  __shared__ wscratch s;
-  if (b.n_jobs == 0) {
-    if (threadIdx.x == 0) w.flags[0] = 0u;
-    return;
-  }
-  const bool one = w_final_exp_is_one(w.f_batch[0], &s);
-  if (threadIdx.x == 0) w.flags[0] = one ? 1u : 0u;
-}
-
-// ------------------------------------------------------------ k_job_final
-__global__ void BGV_BULK k_job_final(dev_batch b, dev_work w) {
-  const uint32_t j = gtid();
-  if (j >= b.n_jobs) return;
-  const int32_t code = w.job_code[j];
-  int32_t res;
-  if (code != C_OK) {
-    res = -code;
-  } else if (w.flags[0]) {
-    res = 1;  // whole batch verified: every job is valid
-  } else {
-    fp12_t r;
-    fp12_final_exp(r, w.f_job[j]);
-    res = fp12_is_one(r) ? 1 : 0;
-  }
-  w.job_result[j] = res;
-}
-
 // set codes for the host: signature code first, then the pubkey code
 __global__ void BGV_BULK k_set_codes(dev_batch b, dev_work w) {
   const uint32_t i = gtid();
   if (i >= b.n_sets) return;
   const int32_t c = w.sig_code[i];
   w.set_code[i] = c != C_OK ? c : w.pk_code[i];
-}
-
-// ------------------------------------------------- multi-GPU combination
-__global__ void BGV_BULK k_combine_final(const fp12_t* parts, uint32_t n, uint32_t* flag) {
-  __shared__ wscratch s;
-  __shared__ fp12_t g;
-  if (threadIdx.x == 0) {
-    fp12_one(g);
-    for (uint32_t k = 0; k < n; k++) fp12_mul(g, g, parts[k]);
-  }
-  __syncthreads();
-  const bool one = w_final_exp_is_one(g, &s);
-  if (threadIdx.x == 0) flag[0] = one ? 1u : 0u;
 }
 
 // Montgomery <-> plain limbs for Fp12 values crossing the host boundary
@@ -684,22 +633,18 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       BGV_LAUNCH(k_miller, b.n_sets / b.pairs_per_item + 2 * b.n_jobs, b, w);  // >= items + jobs
       break;
     case ST_F_TREE:
-      for (uint32_t s = 1; s < span; s *= 2) BGV_LAUNCH(k_f_level, b.n_sets, b, w, s);
-      BGV_LAUNCH(k_job_f, b.n_jobs, b, w, span);
+      launch_fp12_tail(st, stage, b, w);  // bgv_tail.hip
       break;
     case ST_BATCH_PROD:
-      for (uint32_t s = 1; s < b.n_jobs; s *= 2) BGV_LAUNCH(k_batch_level, b.n_jobs, b, w, s);
+      launch_fp12_tail(st, stage, b, w);
       break;
-    case ST_BATCH_FINAL: hipLaunchKernelGGL(k_batch_final, dim3(1), dim3(64), 0, st, b, w); break;
-    case ST_JOB_FINAL: BGV_LAUNCH(k_job_final, b.n_jobs, b, w); break;
+    case ST_BATCH_FINAL:
+    case ST_JOB_FINAL: launch_fp12_tail(st, stage, b, w); break;
     case ST_SET_CODES: BGV_LAUNCH(k_set_codes, b.n_sets, b, w); break;
     default: break;
   }
 }
 
-void launch_combine_final(hipStream_t st, const fp12_t* parts, uint32_t n, uint32_t* flag) {
-  hipLaunchKernelGGL(k_combine_final, dim3(1), dim3(64), 0, st, parts, n, flag);
-}
 void launch_fp12_convert(hipStream_t st, const fp12_t* in, fp12_t* out, uint32_t n, bool to_mont) {
   BGV_LAUNCH(k_fp12_convert, n, in, out, n, to_mont ? 1u : 0u);
 }

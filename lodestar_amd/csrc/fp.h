@@ -111,11 +111,32 @@ BGV_HD void fp_mul32(fp_t& r, const fp_t& a, const fp_t& b);
 #ifndef BGV_FPMUL28
 #define BGV_FPMUL28 1
 #endif
+// BGV_FPMUL_CALL=1: on the device, every product is a call to ONE non-inlined
+// leaf whose operands and result are 12-element vectors, which the AMDGPU
+// calling convention keeps in VGPRs (v0-v23 in, v0-v11 out).  By-reference or
+// struct arguments would travel through the scratch stack.
+#ifndef BGV_FPMUL_CALL
+#define BGV_FPMUL_CALL 0
+#endif
+#if defined(__HIPCC__) && BGV_FPMUL_CALL
+typedef uint32_t fp_vec_t __attribute__((ext_vector_type(12)));
+static __device__ __noinline__ fp_vec_t fp_mul_leaf(fp_vec_t a, fp_vec_t b);
+#endif
 BGV_HD void fp_mul(fp_t& r, const fp_t& a, const fp_t& b) {
 #ifdef BGV_COUNT_OPS
   bgv_fpmul_count++;
 #endif
-#if BGV_FPMUL28
+#if defined(__HIP_DEVICE_COMPILE__) && BGV_FPMUL_CALL
+  fp_vec_t va, vb;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    va[i] = a.l[i];
+    vb[i] = b.l[i];
+  }
+  const fp_vec_t vr = fp_mul_leaf(va, vb);
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.l[i] = vr[i];
+#elif BGV_FPMUL28
   fp_mul28(r, a, b);
 #else
   fp_mul32(r, a, b);
@@ -232,6 +253,22 @@ BGV_HD void fp_mul28(fp_t& r, const fp_t& a, const fp_t& b) {
   pack28(t, d);
   fp_reduce_once(r, t);
 }
+
+#if defined(__HIPCC__) && BGV_FPMUL_CALL
+static __device__ __noinline__ fp_vec_t fp_mul_leaf(fp_vec_t a, fp_vec_t b) {
+  fp_t x, y, r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    x.l[i] = a[i];
+    y.l[i] = b[i];
+  }
+  fp_mul28(r, x, y);
+  fp_vec_t v;
+#pragma unroll
+  for (int i = 0; i < NL; i++) v[i] = r.l[i];
+  return v;
+}
+#endif
 
 BGV_HD void fp_sqr(fp_t& r, const fp_t& a) { fp_mul(r, a, a); }
 
