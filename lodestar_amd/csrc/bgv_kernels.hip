@@ -23,8 +23,9 @@
 //                 multithread/worker.ts:74-85)
 // Code generation of this translation unit (measured on MI355X, r01):
 //  * every Fp product is a call to one non-inlined leaf with its operands in
-//    VGPRs (fp.h BGV_FPMUL_CALL) and the Fp2 layer is inlined, so Fp2
-//    temporaries live in registers instead of on the scratch stack;
+//    VGPRs (fp.h BGV_FPMUL_CALL) and the Fp2 and Fp6 layers are inlined, so
+//    their temporaries live in registers instead of on the scratch stack
+//    (Fp6 inlining: k_miller 33.5 -> 30.5 ms);
 //  * the Miller kernel runs at 1 wave/SIMD: its 512-register budget takes
 //    the spills in AGPRs (k_miller 37.9 -> 33.1 ms at C4).
 // The Fp12 product trees and final exponentiations prefer the inlined
@@ -34,6 +35,9 @@
 #endif
 #ifndef BGV_FP2_INLINE
 #define BGV_FP2_INLINE 1
+#endif
+#ifndef BGV_FP6_INLINE
+#define BGV_FP6_INLINE 1
 #endif
 #ifndef BGV_MILLER_WAVES
 #define BGV_MILLER_WAVES 1
@@ -49,6 +53,18 @@ namespace bgv {
 #define BGV_WAVES 2
 #endif
 #define BGV_BULK __launch_bounds__(64, BGV_WAVES)
+#ifndef BGV_HASH_WAVES
+#define BGV_HASH_WAVES BGV_WAVES
+#endif
+#ifndef BGV_SIG_WAVES
+#define BGV_SIG_WAVES BGV_WAVES
+#endif
+#ifndef BGV_SCALE_WAVES
+#define BGV_SCALE_WAVES BGV_WAVES
+#endif
+#ifndef BGV_PK_WAVES
+#define BGV_PK_WAVES BGV_WAVES
+#endif
 #ifndef BGV_MILLER_WAVES
 #define BGV_MILLER_WAVES BGV_WAVES
 #endif
@@ -116,7 +132,7 @@ __global__ void BGV_BULK k_table_export(const g1a* tab, uint8_t* out96, uint32_t
 }
 
 // ------------------------------------------------------------------ k_sig
-__global__ void BGV_BULK k_sig(dev_batch b, dev_work w) {
+__global__ void __launch_bounds__(64, BGV_SIG_WAVES) k_sig(dev_batch b, dev_work w) {
   const uint32_t i = gtid();
   if (i >= b.n_sets) return;
   const uint32_t len = b.sig_len[i];
@@ -139,7 +155,7 @@ __global__ void BGV_BULK k_sig(dev_batch b, dev_work w) {
 }
 
 // ----------------------------------------------------------------- k_hash
-__global__ void BGV_BULK k_hash(dev_batch b, dev_work w) {
+__global__ void __launch_bounds__(64, BGV_HASH_WAVES) k_hash(dev_batch b, dev_work w) {
   const uint32_t i = gtid();
   if (i >= b.n_sets) return;
   uint8_t m[32];
@@ -208,7 +224,7 @@ __global__ void BGV_BULK k_chunk_set(dev_batch b, dev_work w) {
   for (uint32_t c = w.chunk_off[i]; c < w.chunk_off[i + 1]; c++) w.chunk_set[c] = i;
 }
 
-__global__ void BGV_BULK k_pk_chunk(dev_batch b, dev_work w) {
+__global__ void __launch_bounds__(64, BGV_PK_WAVES) k_pk_chunk(dev_batch b, dev_work w) {
   const uint32_t g = gtid();
   if (g >= w.chunk_off[b.n_sets]) return;
   const uint32_t i = w.chunk_set[g];
@@ -231,7 +247,7 @@ __global__ void BGV_BULK k_pk_chunk(dev_batch b, dev_work w) {
   w.pk_part[g] = acc;
 }
 
-__global__ void BGV_BULK k_pk(dev_batch b, dev_work w) {
+__global__ void __launch_bounds__(64, BGV_PK_WAVES) k_pk(dev_batch b, dev_work w) {
   const uint32_t i = gtid();
   if (i >= b.n_sets) return;
   g1j acc;
@@ -259,7 +275,7 @@ __global__ void BGV_BULK k_pk(dev_batch b, dev_work w) {
 }
 
 // ------------------------------------------------------------ k_sig_scale
-__global__ void BGV_BULK k_sig_scale(dev_batch b, dev_work w) {
+__global__ void __launch_bounds__(64, BGV_SCALE_WAVES) k_sig_scale(dev_batch b, dev_work w) {
   const uint32_t i = gtid();
   if (i >= b.n_sets) return;
   g2j r;

@@ -11,6 +11,17 @@ namespace bgv {
 #ifndef BGV_FP6_INLINE_FP2
 #define BGV_FP6_INLINE_FP2 0
 #endif
+// code-generation knobs (bgv_kernels.hip / bgv_tail.hip pick per unit)
+#if defined(__HIPCC__) && BGV_FP6_INLINE
+#define BGV_NI6 BGV_HD
+#else
+#define BGV_NI6 BGV_NI
+#endif
+#if defined(__HIPCC__) && BGV_FP12_INLINE
+#define BGV_NI12 BGV_HD
+#else
+#define BGV_NI12 BGV_NI
+#endif
 #if BGV_FP6_INLINE_FP2
 #define F6_MUL fp2_mul_inl
 #else
@@ -39,7 +50,7 @@ BGV_HD void fp6_mul_v(fp6_t& r, const fp6_t& a) {
 }
 
 // Karatsuba-style, 6 Fp2 products
-BGV_NI void fp6_mul(fp6_t& r, const fp6_t& a, const fp6_t& b) {
+BGV_NI6 void fp6_mul(fp6_t& r, const fp6_t& a, const fp6_t& b) {
   fp2_t t0, t1, t2, s0, s1, u;
   F6_MUL(t0, a.c0, b.c0);
   F6_MUL(t1, a.c1, b.c1);
@@ -77,7 +88,7 @@ BGV_NI void fp6_mul(fp6_t& r, const fp6_t& a, const fp6_t& b) {
 BGV_HD void fp6_sqr(fp6_t& r, const fp6_t& a) { fp6_mul(r, a, a); }
 
 // a * (b0 + b1 v): 5 Fp2 products
-BGV_NI void fp6_mul_01(fp6_t& r, const fp6_t& a, const fp2_t& b0, const fp2_t& b1) {
+BGV_NI6 void fp6_mul_01(fp6_t& r, const fp6_t& a, const fp2_t& b0, const fp2_t& b1) {
   fp2_t t0, t1, u, s0, s1, c0, c1, c2;
   F6_MUL(t0, a.c0, b0);
   F6_MUL(t1, a.c1, b1);
@@ -98,7 +109,7 @@ BGV_NI void fp6_mul_01(fp6_t& r, const fp6_t& a, const fp2_t& b0, const fp2_t& b
 }
 
 // a * (b1 v): 3 Fp2 products
-BGV_NI void fp6_mul_1(fp6_t& r, const fp6_t& a, const fp2_t& b1) {
+BGV_NI6 void fp6_mul_1(fp6_t& r, const fp6_t& a, const fp2_t& b1) {
   fp2_t c0, c1, c2;
   F6_MUL(c0, a.c2, b1);
   fp2_mul_xi(c0, c0);
@@ -159,7 +170,7 @@ BGV_NI void fp12_mul(fp12_t& r, const fp12_t& a, const fp12_t& b) {
 }
 
 // complex squaring: (a0 + a1 w)^2 = (a0^2 + v a1^2) + 2 a0 a1 w, 2 Fp6 products
-BGV_NI void fp12_sqr(fp12_t& r, const fp12_t& a) {
+BGV_NI12 void fp12_sqr(fp12_t& r, const fp12_t& a) {
   fp6_t t0, t1, t2;
   fp6_mul(t0, a.c0, a.c1);          // a0 a1
   fp6_add(t1, a.c0, a.c1);          // a0 + a1
@@ -173,7 +184,7 @@ BGV_NI void fp12_sqr(fp12_t& r, const fp12_t& a) {
 }
 
 // multiply by a sparse line  l = a0 + a1 w^2 + b1 w^3  (tower: c0 = (a0, a1, 0), c1 = (0, b1, 0))
-BGV_NI void fp12_mul_line(fp12_t& r, const fp12_t& f, const fp2_t& a0, const fp2_t& a1, const fp2_t& b1) {
+BGV_NI12 void fp12_mul_line(fp12_t& r, const fp12_t& f, const fp2_t& a0, const fp2_t& a1, const fp2_t& b1) {
   fp6_t t0, t1, s;
   fp6_mul_01(t0, f.c0, a0, a1);
   fp6_mul_1(t1, f.c1, b1);

@@ -8,12 +8,18 @@
 #pragma once
 #include "h2c.h"
 
+#if defined(__HIPCC__) && BGV_STEP_INLINE
+#define BGV_NIS BGV_HD
+#else
+#define BGV_NIS BGV_NI
+#endif
+
 namespace bgv {
 
 struct g2p_t { fp2_t x, y, z; };  // homogeneous projective: x = X/Z, y = Y/Z
 
 // T <- 2T, line tangent at T evaluated at P
-BGV_NI void miller_dbl_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const fp_t& xp, const fp_t& yp) {
+BGV_NIS void miller_dbl_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const fp_t& xp, const fp_t& yp) {
   fp2_t A, B, C, E, F, G, H, t;
   fp2_mul(A, T.x, T.y);
   fp_half(A.c0, A.c0);
@@ -47,7 +53,7 @@ BGV_NI void miller_dbl_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const fp_
 }
 
 // T <- T + Q (Q affine), line through T and Q evaluated at P
-BGV_NI void miller_add_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const g2a& Q, const fp_t& xp,
+BGV_NIS void miller_add_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const g2a& Q, const fp_t& xp,
                             const fp_t& yp) {
   fp2_t th, la, C, D, E, F, G, H, t;
   fp2_mul(t, Q.y, T.z);
