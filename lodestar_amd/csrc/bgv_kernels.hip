@@ -42,6 +42,9 @@
 #ifndef BGV_MILLER_WAVES
 #define BGV_MILLER_WAVES 1
 #endif
+#ifndef BGV_MILLER_LDS_F
+#define BGV_MILLER_LDS_F 1
+#endif
 #include "bgv_internal.h"
 #include "miller_coop.h"
 
@@ -361,7 +364,15 @@ __global__ void __launch_bounds__(64, BGV_MILLER_WAVES) k_miller(dev_batch b, de
   const uint32_t t = gtid();
   const uint32_t n_items = w.item_off[b.n_jobs];
   if (t >= n_items + b.n_jobs) return;
+  // the accumulator lives in LDS: at 1 wave/SIMD a lane has 640 B of it, and
+  // every fp12_sqr / fp12_mul_line call reads and writes f by reference, which
+  // from a stack slot would be ~3 KB of scratch traffic per lane per bit
+#if BGV_MILLER_LDS_F
+  __shared__ fp12_t f_lds[64];
+  fp12_t& f = f_lds[threadIdx.x];
+#else
   fp12_t f;
+#endif
   if (t < n_items) {
     const uint32_t j = w.item_job[t];
     const uint32_t i1 = b.job_off[j] + b.pairs_per_item * (t - w.item_off[j]);
