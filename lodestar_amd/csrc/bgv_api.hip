@@ -85,7 +85,7 @@ struct bgv_ctx {
   dbuf<uint32_t> chunk_off, chunk_set;
   dbuf<g1j> pk_part;
   dbuf<g2j> rsig;
-  dbuf<fp12_t> f_set, f_job, f_batch, f_part;
+  dbuf<fp12_t> f_set, f_job, f_batch, f_tmp, f_part;
   dbuf<uint32_t> set_job, s_inf, item_off, item_job;
   dbuf<g2a> s_aff;
   // microbench scratch
@@ -116,9 +116,10 @@ const char* bgv_set_code_name(int code) {
 }
 
 const char* bgv_stage_name(int stage) {
-  static const char* names[ST_COUNT] = {"sig_decode_subgroup", "hash_to_g2",    "pk_aggregate_scale", "sig_scale",
-                                        "sig_sum_tree",        "miller_loop",   "miller_product_tree", "batch_product",
-                                        "batch_final_exp",     "job_final_exp", "set_codes"};
+  static const char* names[ST_COUNT] = {"sig_decode_subgroup", "hash_to_g2",          "pk_aggregate_scale",
+                                        "sig_scale",           "sig_sum_tree",        "miller_loop",
+                                        "miller_loop_jobs",    "miller_product_tree", "batch_product",
+                                        "batch_final_exp",     "job_final_exp",       "set_codes"};
   return (stage >= 0 && stage < ST_COUNT) ? names[stage] : "unknown";
 }
 
@@ -133,9 +134,15 @@ int bgv_open(int device, bgv_ctx** out) {
   c->device = device;
   if (const char* m = getenv("BGV_MILLER")) c->miller_mode = strcmp(m, "serial") != 0 ? 1 : 0;
   if (const char* o = getenv("BGV_OVERLAP")) c->overlap = strcmp(o, "0") != 0;
-  HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&c->st_hash, hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&c->st_pk, hipStreamNonBlocking));
+  // hash -> set-pair Miller is the critical path: its stream (and the pubkey
+  // stream feeding it) get the highest priority, signature decode/scaling the
+  // lowest (it only feeds the signature tree and the 1 pair per job)
+  int prio_lo = 0, prio_hi = 0;
+  HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+  if (const char* p = getenv("BGV_PRIO")) if (strcmp(p, "0") == 0) prio_hi = prio_lo;
+  HIPCHK(hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, prio_lo));
+  HIPCHK(hipStreamCreateWithPriority(&c->st_hash, hipStreamNonBlocking, prio_hi));
+  HIPCHK(hipStreamCreateWithPriority(&c->st_pk, hipStreamNonBlocking, prio_hi));
   for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
   for (auto& e : c->ev_end) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipEventCreate(&c->ev_fork));
@@ -159,7 +166,7 @@ int bgv_close(bgv_ctx* c) {
   c->scalars.release(); c->raw_conv.release();
   c->sig_aff.release(); c->h_aff.release(); c->sig_inf.release(); c->flags.release();
   c->sig_code.release(); c->pk_code.release(); c->job_code.release(); c->job_result.release(); c->set_code.release();
-  c->rpk_aff.release(); c->chunk_off.release(); c->chunk_set.release(); c->pk_part.release(); c->rsig.release(); c->f_set.release(); c->f_job.release(); c->f_batch.release(); c->f_part.release();
+  c->rpk_aff.release(); c->chunk_off.release(); c->chunk_set.release(); c->pk_part.release(); c->rsig.release(); c->f_set.release(); c->f_job.release(); c->f_batch.release(); c->f_tmp.release(); c->f_part.release();
   c->set_job.release(); c->s_inf.release(); c->item_off.release(); c->item_job.release(); c->s_aff.release();
   c->mb_fp.release(); c->mb_u64.release();
   (void)hipStreamDestroy(c->st);
@@ -343,7 +350,7 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
   if ((r = c->sig_aff.ensure(ns)) || (r = c->h_aff.ensure(ns)) || (r = c->sig_inf.ensure(ns)) ||
       (r = c->sig_code.ensure(ns)) || (r = c->pk_code.ensure(ns)) || (r = c->rpk_aff.ensure(ns)) ||
       (r = c->rsig.ensure(ns)) || (r = c->f_set.ensure(ns + nj)) || (r = c->set_code.ensure(ns)) ||
-      (r = c->set_job.ensure(ns)) || (r = c->item_off.ensure(nj + 1)) || (r = c->item_job.ensure(ns + nj + 1)) || (r = c->f_job.ensure(nj)) || (r = c->f_batch.ensure(nj)) ||
+      (r = c->set_job.ensure(ns)) || (r = c->item_off.ensure(nj + 1)) || (r = c->item_job.ensure(ns + nj + 1)) || (r = c->f_job.ensure(nj)) || (r = c->f_batch.ensure(nj)) || (r = c->f_tmp.ensure(nj / 32 + 1)) ||
       (r = c->s_aff.ensure(nj)) || (r = c->s_inf.ensure(nj)) || (r = c->job_code.ensure(nj)) ||
       (r = c->job_result.ensure(nj)) || (r = c->f_part.ensure(4)) || (r = c->flags.ensure(4)))
     return r;
@@ -352,18 +359,25 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
   w.set_code = c->set_code.p; w.f_job = c->f_job.p; w.job_code = c->job_code.p; w.job_result = c->job_result.p;
   w.f_part = c->f_part.p; w.flags = c->flags.p;
   w.item_off = c->item_off.p; w.item_job = c->item_job.p;
-  w.set_job = c->set_job.p; w.f_batch = c->f_batch.p; w.s_aff = c->s_aff.p; w.s_inf = c->s_inf.p;
+  w.set_job = c->set_job.p; w.f_batch = c->f_batch.p; w.f_tmp = c->f_tmp.p; w.s_aff = c->s_aff.p; w.s_inf = c->s_inf.p;
   return 0;
 }
 
 // run stages [from, to) with an event before each
-// The three input stages are independent: signature decode (+ its scaling),
-// hash_to_G2 and pubkey aggregation read disjoint inputs and write disjoint
-// buffers (bgv_kernels.hip), so they run on three streams and join before the
-// signature tree.  Each on its own leaves SIMDs idle (1.5 waves per SIMD at C4,
-// ~60% VALU busy); together they fill the gaps.
+// Stage graph on three streams (the stages read disjoint inputs and write
+// disjoint buffers, bgv_kernels.hip):
+//   st      : sig -> sig_scale -> [pk] sig_sum_tree -> miller_loop_jobs -> [miller] tail
+//   st_hash : hash -> [pk] miller_loop (the set pairs)
+//   st_pk   : pk
+// The set-pair Miller loops need only H(m) and the aggregated keys, so they
+// start while the signatures are still being scaled: at C4 the Miller kernel
+// fills 78% of the SIMDs (one wave each) and sig_scale takes the rest.
 static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int from, int to) {
-  const bool fork = c->overlap && from <= ST_SIG && to > ST_S_TREE;
+  const bool fork = c->overlap && from <= ST_SIG && to > ST_F_TREE;
+  if (from <= ST_PK) {
+    launch_prep(c->st, d, w);
+    HIPCHK(hipGetLastError());
+  }
   if (fork) {
     HIPCHK(hipEventRecord(c->ev_fork, c->st));
     HIPCHK(hipStreamWaitEvent(c->st_hash, c->ev_fork, 0));
@@ -371,11 +385,11 @@ static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int fro
   }
   for (int s = from; s < to; s++) {
     hipStream_t st = c->st;
-    if (fork && s == ST_HASH) st = c->st_hash;
-    if (fork && s == ST_PK) st = c->st_pk;
-    if (fork && s == ST_S_TREE) {
-      HIPCHK(hipStreamWaitEvent(c->st, c->ev_end[ST_HASH], 0));
-      HIPCHK(hipStreamWaitEvent(c->st, c->ev_end[ST_PK], 0));
+    if (fork) {
+      if (s == ST_HASH || s == ST_MILLER) st = c->st_hash;
+      if (s == ST_PK) st = c->st_pk;
+      if (s == ST_S_TREE || s == ST_MILLER) HIPCHK(hipStreamWaitEvent(st, c->ev_end[ST_PK], 0));
+      if (s == ST_F_TREE) HIPCHK(hipStreamWaitEvent(st, c->ev_end[ST_MILLER], 0));
     }
     HIPCHK(hipEventRecord(c->ev[s], st));
     launch_stage(st, s, d, w);

@@ -49,7 +49,8 @@ struct dev_work {
   uint32_t* s_inf;
   fp12_t* f_set;      // per pair Miller value: n_sets set pairs, then n_jobs (-G1, S_job) pairs
   fp12_t* f_job;      // per-job Miller product (incl. the -G1 pair)
-  fp12_t* f_batch;    // batch product tree scratch [n_jobs]
+  fp12_t* f_batch;    // batch product scratch [n_jobs]; the product ends in f_batch[0]
+  fp12_t* f_tmp;      // batch fold ping-pong [ceil(n_jobs / 32)]
   int32_t* job_code;
   int32_t* job_result;
   int32_t* set_code;
@@ -64,6 +65,7 @@ enum Stage {
   ST_SIG_SCALE,
   ST_S_TREE,
   ST_MILLER,
+  ST_MILLER_JOBS,
   ST_F_TREE,
   ST_BATCH_PROD,
   ST_BATCH_FINAL,
@@ -76,6 +78,7 @@ void launch_raw_pks(hipStream_t st, const uint8_t* raw, g1a* out, uint32_t n);
 void launch_table_from_compressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n);
 void launch_table_from_uncompressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n);
 void launch_table_export(hipStream_t st, const g1a* tab, uint8_t* out, uint32_t n);
+void launch_prep(hipStream_t st, const dev_batch& b, const dev_work& w);  // before ST_PK / ST_MILLER
 void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work& w);
 void launch_fp12_tail(hipStream_t st, int stage, const dev_batch& b, const dev_work& w);  // bgv_tail.hip
 void launch_combine_final(hipStream_t st, const fp12_t* parts, uint32_t n, uint32_t* flag);

@@ -360,10 +360,10 @@ __global__ void BGV_BULK k_item_job(dev_batch b, dev_work w) {
   for (uint32_t t = w.item_off[j]; t < w.item_off[j + 1]; t++) w.item_job[t] = j;
 }
 
-__global__ void __launch_bounds__(64, BGV_MILLER_WAVES) k_miller(dev_batch b, dev_work w) {
-  const uint32_t t = gtid();
+__global__ void __launch_bounds__(64, BGV_MILLER_WAVES) k_miller(dev_batch b, dev_work w, uint32_t jobs_part) {
   const uint32_t n_items = w.item_off[b.n_jobs];
-  if (t >= n_items + b.n_jobs) return;
+  const uint32_t t = gtid() + (jobs_part ? n_items : 0u);
+  if (jobs_part ? t >= n_items + b.n_jobs : t >= n_items) return;
   // the accumulator lives in LDS: at 1 wave/SIMD a lane has 640 B of it, and
   // every fp12_sqr / fp12_mul_line call reads and writes f by reference, which
   // from a stack slot would be ~3 KB of scratch traffic per lane per bit
@@ -377,9 +377,10 @@ __global__ void __launch_bounds__(64, BGV_MILLER_WAVES) k_miller(dev_batch b, de
     const uint32_t j = w.item_job[t];
     const uint32_t i1 = b.job_off[j] + b.pairs_per_item * (t - w.item_off[j]);
     const bool two = b.pairs_per_item == 2 && i1 + 1 < b.job_off[j + 1];
-    const bool ok1 = w.sig_code[i1] == C_OK && w.pk_code[i1] == C_OK;
-    const bool ok2 = !two || (w.sig_code[i1 + 1] == C_OK && w.pk_code[i1 + 1] == C_OK);
-    // a parse error rejects the whole job, so its Miller values are never used
+    const bool ok1 = w.pk_code[i1] == C_OK;
+    const bool ok2 = !two || w.pk_code[i1 + 1] == C_OK;
+    // a parse error rejects the whole job, so its Miller values are never used;
+    // signature codes are not known yet (this part overlaps ST_SIG_SCALE)
     if (!ok1 || !ok2) fp12_one(f);
     else if (two) miller_loop2(f, w.rpk_aff[i1], w.h_aff[i1], w.rpk_aff[i1 + 1], w.h_aff[i1 + 1]);
     else miller_loop(f, w.rpk_aff[i1], false, w.h_aff[i1], false);
@@ -401,18 +402,20 @@ __global__ void __launch_bounds__(64, BGV_MILLER_WAVES) k_miller(dev_batch b, de
 
 // Cooperative variant (miller_coop.h): 10 pairs per 64-lane workgroup, six
 // lanes per pair, pair t < n_sets is (r_t PK_t, H(m_t)), then (-G1, S_job).
-__global__ void __launch_bounds__(64, BGV_WAVES) k_miller_coop(dev_batch b, dev_work w) {
+__global__ void __launch_bounds__(64, BGV_WAVES) k_miller_coop(dev_batch b, dev_work w, uint32_t first, uint32_t count) {
   __shared__ coop_grp sm[COOP_GROUPS];
   const uint32_t lane = threadIdx.x, grp = lane / COOP_LANES, k = lane % COOP_LANES;
-  const uint32_t t = blockIdx.x * COOP_GROUPS + grp;
-  const uint32_t n_pairs = b.n_sets + b.n_jobs;
-  const bool in_range = grp < COOP_GROUPS && t < n_pairs;
+  const uint32_t t = first + blockIdx.x * COOP_GROUPS + grp;
+  const bool in_range = grp < COOP_GROUPS && t < first + count;
   bool active = in_range;
   if (in_range) {
     g1a P;
     g2a Q;
     if (t < b.n_sets) {
-      active = w.sig_code[t] == C_OK && w.pk_code[t] == C_OK;
+      // set pairs run before the signatures are decoded (ST_MILLER overlaps
+      // ST_SIG_SCALE): a job with a bad signature is rejected by its code and
+      // its Miller values are never used
+      active = w.pk_code[t] == C_OK;
       P = w.rpk_aff[t];
       Q = w.h_aff[t];
     } else {
@@ -630,15 +633,27 @@ void launch_table_from_uncompressed(hipStream_t st, const uint8_t* in, g1a* out,
 void launch_table_export(hipStream_t st, const g1a* tab, uint8_t* out, uint32_t n) {
   BGV_LAUNCH(k_table_export, n, tab, out, n);
 }
+// Index-only set-up of ST_PK (balanced 32-key chunks) and ST_MILLER (work
+// items): launched before the stages fork onto their streams, while the GPU
+// is idle.  Under the bulk kernels the one-workgroup scan is starved of its
+// CU (rocprofv3: 20 ms instead of tens of microseconds).
+void launch_prep(hipStream_t st, const dev_batch& b, const dev_work& w) {
+  BGV_LAUNCH(k_chunk_count, b.n_sets, b, w);
+  if (b.n_sets) hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, w.chunk_off, b.n_sets);
+  BGV_LAUNCH(k_chunk_set, b.n_sets, b, w);
+  if (!b.miller_coop) {
+    BGV_LAUNCH(k_item_count, b.n_jobs, b, w);
+    if (b.n_jobs) hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, w.item_off, b.n_jobs);
+    BGV_LAUNCH(k_item_job, b.n_jobs, b, w);
+  }
+}
+
 void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work& w) {
   const uint32_t span = 1u << b.span_log2;
   switch (stage) {
     case ST_SIG: BGV_LAUNCH(k_sig, b.n_sets, b, w); break;
     case ST_HASH: BGV_LAUNCH(k_hash, b.n_sets, b, w); break;
-    case ST_PK:
-      BGV_LAUNCH(k_chunk_count, b.n_sets, b, w);
-      if (b.n_sets) hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, w.chunk_off, b.n_sets);
-      BGV_LAUNCH(k_chunk_set, b.n_sets, b, w);
+    case ST_PK:  // after launch_prep
       BGV_LAUNCH(k_pk_chunk, b.chunk_bound, b, w);
       BGV_LAUNCH(k_pk, b.n_sets, b, w);
       break;
@@ -648,16 +663,21 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       for (uint32_t s = 1; s < span; s *= 2) BGV_LAUNCH(k_s_level, b.n_sets, b, w, s);
       BGV_LAUNCH(k_job_s, b.n_jobs, b, w, span);
       break;
-    case ST_MILLER:
+    case ST_MILLER:  // (r_i PK_i, H(m_i)) pairs: needs ST_HASH and ST_PK only
       if (b.miller_coop) {
-        const uint32_t pairs = b.n_sets + b.n_jobs;
-        if (pairs) hipLaunchKernelGGL(k_miller_coop, dim3((pairs + COOP_GROUPS - 1) / COOP_GROUPS), dim3(64), 0, st, b, w);
+        if (b.n_sets)
+          hipLaunchKernelGGL(k_miller_coop, dim3((b.n_sets + COOP_GROUPS - 1) / COOP_GROUPS), dim3(64), 0, st, b, w, 0u, b.n_sets);
         break;
       }
-      BGV_LAUNCH(k_item_count, b.n_jobs, b, w);
-      if (b.n_jobs) hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, w.item_off, b.n_jobs);
-      BGV_LAUNCH(k_item_job, b.n_jobs, b, w);
-      BGV_LAUNCH(k_miller, b.n_sets / b.pairs_per_item + 2 * b.n_jobs, b, w);  // >= items + jobs
+      BGV_LAUNCH(k_miller, b.n_sets / b.pairs_per_item + b.n_jobs, b, w, 0u);  // >= items (launch_prep)
+      break;
+    case ST_MILLER_JOBS:  // (-G1, S_job) pairs: needs ST_S_TREE
+      if (b.miller_coop) {
+        if (b.n_jobs)
+          hipLaunchKernelGGL(k_miller_coop, dim3((b.n_jobs + COOP_GROUPS - 1) / COOP_GROUPS), dim3(64), 0, st, b, w, b.n_sets, b.n_jobs);
+        break;
+      }
+      BGV_LAUNCH(k_miller, b.n_jobs, b, w, 1u);
       break;
     case ST_F_TREE:
       launch_fp12_tail(st, stage, b, w);  // bgv_tail.hip

@@ -12,7 +12,7 @@
 #define BGV_FPMUL_CALL 0
 #endif
 #include "bgv_internal.h"
-#include "fp12_wave.h"
+#include "fp12_coop.h"
 
 namespace bgv {
 
@@ -20,7 +20,6 @@ namespace bgv {
 #define BGV_TREE_WAVES 2
 #endif
 #define BGV_TREE_LB __launch_bounds__(64, BGV_TREE_WAVES)
-#define BGV_BULK BGV_TREE_LB
 
 __device__ __forceinline__ static uint32_t tree_gtid() { return blockIdx.x * blockDim.x + threadIdx.x; }
 #define gtid tree_gtid
@@ -55,30 +54,60 @@ __global__ void BGV_TREE_LB k_job_f(dev_batch b, dev_work w, uint32_t span) {
   w.f_batch[j] = f;
 }
 
-// ---------------------------------------------------------- batch product
-__global__ void BGV_TREE_LB k_batch_level(dev_batch b, dev_work w, uint32_t s) {
-  const uint32_t j = gtid();
-  if (j >= b.n_jobs || (j % (2 * s)) != 0 || j + s >= b.n_jobs) return;
-  fp12_t a = w.f_batch[j];
-  fp12_mul(a, a, w.f_batch[j + s]);
-  w.f_batch[j] = a;
+// ------------------------------------------- cooperative folds (fp12_coop.h)
+#define COOP_LB __launch_bounds__(COOP_THREADS, 2)
+
+// one workgroup per job: f_job = (job pair value) * prod of the job's set
+// values, folded in order at the latency of one Fp product per step
+__global__ void COOP_LB k_job_fold(dev_batch b, dev_work w) {
+  __shared__ cscratch s;
+  __shared__ wfp12 acc, x;
+  const uint32_t j = blockIdx.x;
+  const uint32_t beg = b.job_off[j], end = b.job_off[j + 1];
+  if (w.job_code[j] != C_OK) {
+    c_set_one(&acc);  // rejected jobs take no part in the batch product
+  } else {
+    c_load(&acc, w.f_set[b.n_sets + j]);
+    for (uint32_t i = beg; i < end; i++) {
+      c_load(&x, w.f_set[i]);
+      c_mul(&acc, &acc, &x, &s);
+    }
+  }
+  c_store(w.f_job[j], &acc);
+  c_store(w.f_batch[j], &acc);
 }
 
-// the whole-batch check: ONE final exponentiation, wave-cooperative (fp12_wave.h)
-__global__ void BGV_BULK k_batch_final(dev_batch b, dev_work w) {
-  __shared__ wscratch s;
+// workgroup g: dst[g] = prod src[32 g .. min(n, 32 g + 32)); with one
+// workgroup dst may alias src (every read precedes the write)
+__global__ void COOP_LB k_fold32(const fp12_t* src, uint32_t n, fp12_t* dst) {
+  __shared__ cscratch s;
+  __shared__ wfp12 acc, x;
+  const uint32_t beg = blockIdx.x * 32u, end = min(n, beg + 32u);
+  c_load(&acc, src[beg]);
+  for (uint32_t i = beg + 1; i < end; i++) {
+    c_load(&x, src[i]);
+    c_mul(&acc, &acc, &x, &s);
+  }
+  c_store(dst[blockIdx.x], &acc);
+}
+
+// the whole-batch check: ONE final exponentiation over 128 lanes
+__global__ void COOP_LB k_batch_final(dev_batch b, dev_work w) {
+  __shared__ cscratch s;
   if (b.n_jobs == 0) {
     if (threadIdx.x == 0) w.flags[0] = 0u;
     return;
   }
-  const bool one = w_final_exp_is_one(w.f_batch[0], &s);
+  const bool one = c_final_exp_is_one(w.f_batch[0], &s);
   if (threadIdx.x == 0) w.flags[0] = one ? 1u : 0u;
 }
 
-// ------------------------------------------------------------ k_job_final
-__global__ void BGV_BULK k_job_final(dev_batch b, dev_work w) {
-  const uint32_t j = gtid();
-  if (j >= b.n_jobs) return;
+// per-job verdicts; a final exponentiation per job only when the batch check
+// failed (the worker's per-job retry, multithread/worker.ts:74-85), one
+// workgroup per job
+__global__ void COOP_LB k_job_final(dev_batch b, dev_work w) {
+  __shared__ cscratch s;
+  const uint32_t j = blockIdx.x;
   const int32_t code = w.job_code[j];
   int32_t res;
   if (code != C_OK) {
@@ -86,23 +115,23 @@ __global__ void BGV_BULK k_job_final(dev_batch b, dev_work w) {
   } else if (w.flags[0]) {
     res = 1;  // whole batch verified: every job is valid
   } else {
-    fp12_t r;
-    fp12_final_exp(r, w.f_job[j]);
-    res = fp12_is_one(r) ? 1 : 0;
+    res = c_final_exp_is_one(w.f_job[j], &s) ? 1 : 0;
   }
-  w.job_result[j] = res;
+  if (threadIdx.x == 0) w.job_result[j] = res;
 }
 
 // ------------------------------------------------- multi-GPU combination
-__global__ void BGV_BULK k_combine_final(const fp12_t* parts, uint32_t n, uint32_t* flag) {
-  __shared__ wscratch s;
+__global__ void COOP_LB k_combine_final(const fp12_t* parts, uint32_t n, uint32_t* flag) {
+  __shared__ cscratch s;
+  __shared__ wfp12 acc, x;
   __shared__ fp12_t g;
-  if (threadIdx.x == 0) {
-    fp12_one(g);
-    for (uint32_t k = 0; k < n; k++) fp12_mul(g, g, parts[k]);
+  c_set_one(&acc);
+  for (uint32_t k = 0; k < n; k++) {
+    c_load(&x, parts[k]);
+    c_mul(&acc, &acc, &x, &s);
   }
-  __syncthreads();
-  const bool one = w_final_exp_is_one(g, &s);
+  c_store(g, &acc);
+  const bool one = c_final_exp_is_one(g, &s);
   if (threadIdx.x == 0) flag[0] = one ? 1u : 0u;
 }
 
@@ -111,21 +140,38 @@ __global__ void BGV_BULK k_combine_final(const fp12_t* parts, uint32_t n, uint32
 void launch_fp12_tail(hipStream_t st, int stage, const dev_batch& b, const dev_work& w) {
   const uint32_t span = 1u << b.span_log2;
   auto grid = [](uint32_t n) { return dim3((n + 63u) / 64u); };
+  const dim3 ct(COOP_THREADS);
   if (stage == ST_F_TREE) {
+    if (!b.n_jobs) return;
+    if (span <= 256) {  // every job folds in one workgroup
+      hipLaunchKernelGGL(k_job_fold, dim3(b.n_jobs), ct, 0, st, b, w);
+      return;
+    }
+    // larger jobs: segmented pairwise tree first
     if (b.n_sets)
       for (uint32_t s = 1; s < span; s *= 2) hipLaunchKernelGGL(k_f_level, grid(b.n_sets), dim3(64), 0, st, b, w, s);
-    if (b.n_jobs) hipLaunchKernelGGL(k_job_f, grid(b.n_jobs), dim3(64), 0, st, b, w, span);
+    hipLaunchKernelGGL(k_job_f, grid(b.n_jobs), dim3(64), 0, st, b, w, span);
   } else if (stage == ST_BATCH_PROD) {
-    for (uint32_t s = 1; s < b.n_jobs; s *= 2) hipLaunchKernelGGL(k_batch_level, grid(b.n_jobs), dim3(64), 0, st, b, w, s);
+    // fold by 32, ping-ponging f_batch <-> f_tmp, the product landing in f_batch[0]
+    uint32_t n = b.n_jobs;
+    fp12_t* src = w.f_batch;
+    while (n > 32) {
+      fp12_t* dst = src == w.f_batch ? w.f_tmp : w.f_batch;
+      const uint32_t groups = (n + 31) / 32;
+      hipLaunchKernelGGL(k_fold32, dim3(groups), ct, 0, st, src, n, dst);
+      src = dst;
+      n = groups;
+    }
+    if (n > 1 || (n == 1 && src != w.f_batch)) hipLaunchKernelGGL(k_fold32, dim3(1), ct, 0, st, src, n, w.f_batch);
   } else if (stage == ST_BATCH_FINAL) {
-    hipLaunchKernelGGL(k_batch_final, dim3(1), dim3(64), 0, st, b, w);
+    hipLaunchKernelGGL(k_batch_final, dim3(1), ct, 0, st, b, w);
   } else if (stage == ST_JOB_FINAL) {
-    if (b.n_jobs) hipLaunchKernelGGL(k_job_final, grid(b.n_jobs), dim3(64), 0, st, b, w);
+    if (b.n_jobs) hipLaunchKernelGGL(k_job_final, dim3(b.n_jobs), ct, 0, st, b, w);
   }
 }
 
 void launch_combine_final(hipStream_t st, const fp12_t* parts, uint32_t n, uint32_t* flag) {
-  hipLaunchKernelGGL(k_combine_final, dim3(1), dim3(64), 0, st, parts, n, flag);
+  hipLaunchKernelGGL(k_combine_final, dim3(1), dim3(COOP_THREADS), 0, st, parts, n, flag);
 }
 
 }  // namespace bgv

@@ -1,0 +1,210 @@
+// Fp12 arithmetic spread over a 128-thread workgroup (two waves), one Fp
+// product per lane: the latency-bound tail of the verifier (per-job folds of
+// the Miller values, the batch product, the final exponentiations) runs at
+// the latency of ONE Fp product per Fp12 multiplication.
+//
+// Same basis as fp12_wave.h: Fp12 = Fp2[w] / (w^6 - xi), w^k coefficient k
+// (tower slot: 0 c0.c0, 1 c1.c0, 2 c0.c1, 3 c1.c1, 4 c0.c2, 5 c1.c2).  A
+// product a * b is the 6 x 6 schoolbook of Fp2 products a_i b_j, each by
+// Karatsuba over three Fp products:
+//   round 1  lane l < 108: pair p = l / 3 (i = p / 6, j = p % 6), Fp product
+//            q = l % 3 of a_i b_j: a0 b0 | a1 b1 | (a0 + a1)(b0 + b1)
+//   round 2  lane l < 36: a_i b_j = (P0 - P1) + (P2 - P0 - P1) i, times xi
+//            when i + j >= 6
+//   round 3  lane l < 12: one Fp component of c_k = sum_i a_i b_(k-i)
+// Every function is called by all 128 threads (it contains __syncthreads()).
+#pragma once
+#include "fp12_wave.h"
+
+namespace bgv {
+
+constexpr uint32_t COOP_THREADS = 128;
+
+struct cscratch {
+  fp_t p[108];
+  fp2_t q[36];
+  wfp12 t[6];  // temporaries of the final exponentiation
+};
+
+// out = a * b (out may alias a or b)
+__device__ void c_mul(wfp12* out, const wfp12* a, const wfp12* b, cscratch* s) {
+  const uint32_t l = threadIdx.x;
+  if (l < 108) {
+    const uint32_t p = l / 3, q = l - 3 * p, i = p / 6, j = p - 6 * i;
+    const fp2_t& x = a->c[i];
+    const fp2_t& y = b->c[j];
+    fp_t u, v;
+    if (q == 0) {
+      u = x.c0;
+      v = y.c0;
+    } else if (q == 1) {
+      u = x.c1;
+      v = y.c1;
+    } else {
+      fp_add(u, x.c0, x.c1);
+      fp_add(v, y.c0, y.c1);
+    }
+    fp_mul(s->p[l], u, v);
+  }
+  __syncthreads();
+  if (l < 36) {
+    const uint32_t i = l / 6, j = l - 6 * i;
+    fp2_t t;
+    fp_t w;
+    fp_sub(t.c0, s->p[3 * l], s->p[3 * l + 1]);
+    fp_add(w, s->p[3 * l], s->p[3 * l + 1]);
+    fp_sub(t.c1, s->p[3 * l + 2], w);
+    if (i + j >= 6) fp2_mul_xi(t, t);
+    s->q[l] = t;
+  }
+  __syncthreads();
+  if (l < 12) {
+    const uint32_t k = l >> 1, comp = l & 1;
+    fp_t acc = comp ? s->q[k].c1 : s->q[k].c0;  // i = 0, j = k
+#pragma unroll
+    for (uint32_t i = 1; i < 6; i++) {
+      const fp2_t& t = s->q[i * 6 + (k + 6 - i) % 6];
+      fp_add(acc, acc, comp ? t.c1 : t.c0);
+    }
+    if (comp) out->c[k].c1 = acc;
+    else out->c[k].c0 = acc;
+  }
+  __syncthreads();
+}
+
+__device__ void c_set_one(wfp12* r) {
+  const uint32_t l = threadIdx.x;
+  if (l < 6) r->c[l] = l == 0 ? fp2_one() : fp2_zero();
+  __syncthreads();
+}
+
+// r = f (tower layout, any address space) in the w basis
+__device__ void c_load(wfp12* r, const fp12_t& f) {
+  const uint32_t l = threadIdx.x;
+  if (l < 6) {
+    const fp6_t& h = (l & 1) ? f.c1 : f.c0;
+    const uint32_t s = l >> 1;
+    r->c[l] = s == 0 ? h.c0 : (s == 1 ? h.c1 : h.c2);
+  }
+  __syncthreads();
+}
+
+__device__ void c_store(fp12_t& f, const wfp12* r) {
+  const uint32_t l = threadIdx.x;
+  if (l < 6) {
+    fp6_t& h = (l & 1) ? f.c1 : f.c0;
+    const uint32_t s = l >> 1;
+    if (s == 0) h.c0 = r->c[l];
+    else if (s == 1) h.c1 = r->c[l];
+    else h.c2 = r->c[l];
+  }
+  __syncthreads();
+}
+
+__device__ void c_copy(wfp12* out, const wfp12* a) {
+  const uint32_t l = threadIdx.x;
+  if (l < 6) out->c[l] = a->c[l];
+  __syncthreads();
+}
+
+__device__ void c_conj(wfp12* out, const wfp12* a) {
+  const uint32_t l = threadIdx.x;
+  if (l < 6) {
+    fp2_t t = a->c[l];
+    if (l & 1) fp2_neg(t, t);
+    out->c[l] = t;
+  }
+  __syncthreads();
+}
+
+// Frobenius pi^k, k = 1..3: lane 2m + c computes component c of coefficient m
+__device__ void c_frob(wfp12* out, const wfp12* a, int k, cscratch* s) {
+  const uint32_t l = threadIdx.x;
+  if (l < 12) {
+    const uint32_t m = l >> 1, comp = l & 1;
+    fp2_t t = a->c[m];
+    if (k & 1) fp2_conj(t, t);
+    fp_t r;
+    if (m == 0) {
+      r = comp ? t.c1 : t.c0;
+    } else {  // (t0 + t1 i)(g0 + g1 i): component comp by two Fp products
+      const fp2_t& g = FROB_G[k - 1][m - 1];
+      fp_t x, y;
+      if (comp == 0) {
+        fp_mul(x, t.c0, g.c0);
+        fp_mul(y, t.c1, g.c1);
+        fp_sub(r, x, y);
+      } else {
+        fp_mul(x, t.c0, g.c1);
+        fp_mul(y, t.c1, g.c0);
+        fp_add(r, x, y);
+      }
+    }
+    s->p[l] = r;
+  }
+  __syncthreads();
+  if (l < 6) {
+    out->c[l].c0 = s->p[2 * l];
+    out->c[l].c1 = s->p[2 * l + 1];
+  }
+  __syncthreads();
+}
+
+// out = a^x (x < 0) for a in the cyclotomic subgroup
+__device__ void c_pow_x(wfp12* out, const wfp12* a, wfp12* acc, cscratch* s) {
+  c_copy(acc, a);
+  for (int b = 62; b >= 0; b--) {
+    c_mul(acc, acc, acc, s);
+    if ((BLS_X_ABS >> b) & 1ull) c_mul(acc, acc, a, s);
+  }
+  c_conj(out, acc);
+}
+
+// Final exponentiation with the addition chain of fp12_final_exp; returns
+// (to every thread) whether f^((p^12 - 1)/r) == 1.
+__device__ bool c_final_exp_is_one(const fp12_t& f_in, cscratch* s) {
+  const uint32_t l = threadIdx.x;
+  wfp12 *t0 = &s->t[0], *t1 = &s->t[1], *y0 = &s->t[2], *y1 = &s->t[3], *y2 = &s->t[4], *acc = &s->t[5];
+  __shared__ wfp12 fin, y3;
+  __shared__ uint32_t result;
+  if (l == 0) {
+    // the one Fp12 inversion of the easy part stays on one lane (its Fp
+    // inversion is a divstep chain, fp.h)
+    fp12_t inv;
+    fp12_inv(inv, f_in);
+    w_from_tower(*t0, inv);
+    w_from_tower(fin, f_in);
+  }
+  __syncthreads();
+  c_conj(t1, &fin);
+  c_mul(t1, t1, t0, s);  // f^(p^6 - 1)
+  c_frob(t0, t1, 2, s);
+  c_mul(t1, t0, t1, s);  // m = f^((p^6-1)(p^2+1))
+  c_pow_x(t0, t1, acc, s);
+  c_conj(y0, t1);
+  c_mul(y0, t0, y0, s);  // m^(x-1)
+  c_pow_x(t0, y0, acc, s);
+  c_conj(y1, y0);
+  c_mul(y1, t0, y1, s);  // m^((x-1)^2)
+  c_pow_x(t0, y1, acc, s);
+  c_frob(y2, y1, 1, s);
+  c_mul(y2, t0, y2, s);  // y1^(x + p)
+  c_pow_x(t0, y2, acc, s);
+  c_pow_x(t0, t0, acc, s);  // y2^(x^2)
+  c_frob(&y3, y2, 2, s);
+  c_mul(&y3, t0, &y3, s);
+  c_conj(t0, y2);
+  c_mul(&y3, &y3, t0, s);  // y2^(x^2 + p^2 - 1)
+  c_mul(t0, t1, t1, s);
+  c_mul(t0, t0, t1, s);  // m^3
+  c_mul(&y3, &y3, t0, s);
+  if (l == 0) {
+    fp12_t r;
+    w_to_tower(r, y3);
+    result = fp12_is_one(r) ? 1u : 0u;
+  }
+  __syncthreads();
+  return result != 0;
+}
+
+}  // namespace bgv

@@ -18,15 +18,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def per_kernel(path, counter):
-    tot, n = defaultdict(float), defaultdict(int)
+    """kernel -> (bytes of its largest-grid dispatch, number of dispatches)"""
+    best, n = {}, defaultdict(int)
     with open(path) as f:
         for row in csv.DictReader(f):
             if row["Counter_Name"] != counter:
                 continue
             name = row["Kernel_Name"].split("(")[0].replace("bgv::", "").strip()
-            tot[name] += float(row["Counter_Value"]) * 1024.0
+            grid, val = int(row["Grid_Size"]), float(row["Counter_Value"]) * 1024.0
             n[name] += 1
-    return tot, n
+            if name not in best or grid > best[name][0]:
+                best[name] = (grid, val)
+    return {k: v[1] for k, v in best.items()}, n
 
 
 def main():
@@ -37,20 +40,19 @@ def main():
     out = {
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bench.py --steps 1 --warmup 0 --no-c2; "
                   f"profiles/{tag}_pmc_fetch_size.csv, profiles/{tag}_pmc_write_size.csv",
-        "note": "per launch; FETCH_SIZE is reported raw (KB x 1024): the gfx950 1/2 under-count the microarch guide documents "
+        "note": "per launch (the kernel's largest-grid dispatch); FETCH_SIZE is reported raw (KB x 1024): the gfx950 1/2 under-count the microarch guide documents "
                 "for 16-B/lane streaming reads is NOT applied (these are scratch accesses, width uncalibrated)",
         "kernels": {},
     }
     for k in sorted(set(fetch) | set(write), key=lambda k: -(fetch.get(k, 0) + write.get(k, 0))):
         if not k.startswith("k_"):
             continue
-        launches = max(nf.get(k, 1), 1)
-        out["kernels"][k] = {"fetch_bytes": fetch.get(k, 0.0) / launches, "write_bytes": write.get(k, 0.0) / launches,
-                             "launches_summed": launches}
+        out["kernels"][k] = {"fetch_bytes": fetch.get(k, 0.0), "write_bytes": write.get(k, 0.0),
+                             "dispatches": nf.get(k, 0), "dispatch": "largest grid"}
     with open(os.path.join(ROOT, "tools", "pmc_traffic.json"), "w") as f:
         json.dump(out, f, indent=1)
     for k, v in list(out["kernels"].items())[:8]:
-        print(f"{k:16s} fetch {v['fetch_bytes'] / 1e9:8.2f} GB  write {v['write_bytes'] / 1e9:8.2f} GB  x{v['launches_summed']}")
+        print(f"{k:16s} fetch {v['fetch_bytes'] / 1e9:8.2f} GB  write {v['write_bytes'] / 1e9:8.2f} GB  ({v['dispatches']} dispatches)")
 
 
 if __name__ == "__main__":
