@@ -44,3 +44,44 @@ def test_two_pair_items_batch_with_faults():
         assert jr2.tolist() == [0 if bad[bounds[i]:bounds[i + 1]].any() else 1 for i in range(4)]
     finally:
         d.close()
+
+
+def test_many_jobs_batch_fold_and_fold_boundary():
+    """2,100 single-set jobs: the batch product folds by 32 three times
+    (2100 -> 66 -> 3 -> 1, ping-ponging f_batch and f_tmp); a job of exactly
+    256 sets is the largest that folds in one workgroup (bgv_tail.hip)."""
+    from lodestar_amd import native
+    d = native.Device(0)
+    try:
+        d.gen_keys(0, 512, 3)
+        rng = np.random.default_rng(5)
+        n, k = 2100, 2
+        idx = rng.integers(0, 512, size=n * k).astype(np.uint32)
+        msgs = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+        arrays = {"n_sets": n, "n_jobs": n, "job_offsets": np.arange(n + 1, dtype=np.uint32),
+                  "pk_offsets": (np.arange(n + 1) * k).astype(np.uint32), "pk_indices": idx, "msgs": msgs}
+        sigs = np.zeros((n, 192), np.uint8)
+        d.gen_sign(arrays, sigs)
+        arrays.update(sigs=sigs, sig_len=np.full(n, 96, np.uint32),
+                      scalars=rng.integers(1, 2**63, size=n, dtype=np.uint64))
+        jr, _ = d.verify(arrays)
+        assert jr.tolist() == [1] * n and d.last_stats.batch_retries == 0
+        good = sigs.copy()
+        bad = [7, 1500, 2099]
+        for i in bad:
+            arrays["sigs"][i] = good[(i + 1) % n]  # a valid signature of another set
+        jr, _ = d.verify(arrays)
+        assert jr.tolist() == [0 if i in bad else 1 for i in range(n)]
+        assert d.last_stats.batch_retries == 1
+        # 256-set job (fold path) + 1844 singles; then a 257-set job (tree path)
+        for first in (256, 257):
+            a2 = dict(arrays, sigs=good.copy())
+            a2["job_offsets"] = np.concatenate([[0], np.arange(first, n + 1)]).astype(np.uint32)
+            a2["n_jobs"] = len(a2["job_offsets"]) - 1
+            jr2, _ = d.verify(a2)
+            assert jr2.tolist() == [1] * a2["n_jobs"]
+            a2["sigs"][first // 2] = good[0]
+            jr2, _ = d.verify(a2)
+            assert jr2.tolist() == [0] + [1] * (a2["n_jobs"] - 1)
+    finally:
+        d.close()
