@@ -52,19 +52,20 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def build_segment(blocks: list[int], seed: int = SEED):
+def build_segment(blocks: list[int], seed: int = SEED, att_per_block: int = ATT_PER_BLOCK):
     """Host arrays for the given block ids of the segment (deterministic per block)."""
     job_off, pk_off, idx, msgs = [0], [0], [], []
+    per_block = att_per_block + SETS_PER_BLOCK - ATT_PER_BLOCK
     perm = np.random.default_rng(seed).permutation(N_VALIDATORS).astype(np.uint32)
     n = 0
     for b in blocks:
         rng = np.random.default_rng([seed, b])
         # attesters of the block: disjoint committees (a slice of a shuffling)
         start = int(rng.integers(0, N_VALIDATORS))
-        att = np.take(perm, np.arange(start, start + ATT_PER_BLOCK * ATT_K) % N_VALIDATORS)
+        att = np.take(perm, np.arange(start, start + att_per_block * ATT_K) % N_VALIDATORS)
         sync = rng.choice(N_VALIDATORS, size=SYNC_K, replace=False).astype(np.uint32)
         singles = rng.integers(0, N_VALIDATORS, size=2).astype(np.uint32)
-        for a in range(ATT_PER_BLOCK):
+        for a in range(att_per_block):
             idx.append(att[a * ATT_K : (a + 1) * ATT_K])
             pk_off.append(pk_off[-1] + ATT_K)
         idx.append(sync)
@@ -72,9 +73,9 @@ def build_segment(blocks: list[int], seed: int = SEED):
         for s in singles:
             idx.append(np.array([s], np.uint32))
             pk_off.append(pk_off[-1] + 1)
-        for k in range(SETS_PER_BLOCK):
-            msgs.append(hashlib.sha256(b"bgv-msg" + seed.to_bytes(8, "little") + (b * SETS_PER_BLOCK + k).to_bytes(4, "little")).digest())
-        n += SETS_PER_BLOCK
+        for k in range(per_block):
+            msgs.append(hashlib.sha256(b"bgv-msg" + seed.to_bytes(8, "little") + (b * per_block + k).to_bytes(4, "little")).digest())
+        n += per_block
         job_off.append(n)
     return {
         "n_sets": n,
@@ -129,6 +130,74 @@ def cpu_baseline(budget_s: float = 10.0):
     return cref.bench_segment_sample(budget_s=budget_s, seed=SEED)
 
 
+def singles(n: int, seed: int):
+    """C1: n single-pubkey sets in one job"""
+    rng = np.random.default_rng(seed)
+    msgs = [hashlib.sha256(b"bgv-msg-c1" + seed.to_bytes(8, "little") + i.to_bytes(4, "little")).digest() for i in range(n)]
+    return {"n_sets": n, "n_jobs": 1, "job_offsets": np.array([0, n], np.uint32),
+            "pk_offsets": np.arange(n + 1, dtype=np.uint32),
+            "pk_indices": rng.integers(0, N_VALIDATORS, size=n).astype(np.uint32),
+            "msgs": np.frombuffer(b"".join(msgs), np.uint8).reshape(n, 32).copy(), "n_raw": 0}
+
+
+def golden_fault_sigs():
+    """96-byte signatures the oracle rejects, from the committed golden vectors
+    (tests/golden/batch_vectors.json, generated by tools/gen_golden.py):
+    on-curve-not-in-G2 (BLST_POINT_NOT_IN_GROUP)."""
+    v = json.load(open(os.path.join(ROOT, "tests", "golden", "batch_vectors.json")))
+    for j in v["jobs"]:
+        for st in j["sets"]:
+            if st.get("code") == 3 and len(st["sig"]) == 192:
+                return bytes.fromhex(st["sig"])
+    raise RuntimeError("no not-in-G2 vector in the golden file")
+
+
+def inject_faults(d, arrays: dict, rate: float, seed: int):
+    """C5: `rate` of the sets faulted, a quarter each of wrong-message
+    signature (-> false), swapped pubkey index (-> false), cleared compression flag
+    (-> reject BLST_BAD_ENCODING) and an on-curve point outside G2 (-> reject
+    BLST_POINT_NOT_IN_GROUP).  Returns (arrays with sigs, expected per-job results)."""
+    n, nj = arrays["n_sets"], arrays["n_jobs"]
+    rng = np.random.default_rng(seed)
+    pick = np.sort(rng.choice(n, size=max(4, int(n * rate)), replace=False))
+    kind = rng.permutation(np.arange(len(pick)) % 4)
+    sign_msgs = arrays["msgs"].copy()
+    sign_msgs[pick[kind == 0], 0] ^= 1
+    sigs = np.zeros((n, 192), np.uint8)
+    d.gen_sign(dict(arrays, msgs=sign_msgs), sigs)
+    out = dict(arrays, pk_indices=arrays["pk_indices"].copy())
+    for i in pick[kind == 1]:
+        o = int(arrays["pk_offsets"][i])
+        out["pk_indices"][o] = (int(out["pk_indices"][o]) + 1) % N_VALIDATORS
+    sigs[pick[kind == 2], 0] &= 0x7F
+    bad_g2 = np.frombuffer(golden_fault_sigs(), np.uint8)
+    sigs[pick[kind == 3], :96] = bad_g2
+    out["sigs"] = sigs
+    out["sig_len"] = np.full(n, 96, np.uint32)
+    code = np.zeros(n, np.int32)
+    code[pick[kind == 2]] = 1
+    code[pick[kind == 3]] = 3
+    false_set = np.zeros(n, bool)
+    false_set[pick[(kind == 0) | (kind == 1)]] = True
+    expect = []
+    jo = arrays["job_offsets"]
+    for j in range(nj):
+        c = code[jo[j]:jo[j + 1]]
+        nz = np.nonzero(c)[0]
+        expect.append(-int(c[nz[0]]) if len(nz) else (0 if false_set[jo[j]:jo[j + 1]].any() else 1))
+    return out, np.array(expect, np.int32)
+
+
+def p50_latency(d, arrays: dict, reps: int = 6):
+    lat = []
+    for _ in range(reps):
+        t1 = time.perf_counter()
+        jr, _ = d.verify(arrays, want_set_codes=False)
+        lat.append((time.perf_counter() - t1) * 1e3)
+        assert (jr == 1).all()
+    return round(float(np.median(lat[1:])), 3)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -136,7 +205,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--blocks", type=int, default=1024, help="blocks in the segment (1024 = 32 epochs)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-c2", action="store_true", help="skip the C2 latency leg (profiling runs)")
+    ap.add_argument("--no-c2", action="store_true", help="skip the C1/C2/C3/C5 legs (profiling runs)")
     args = ap.parse_args()
 
     import torch
@@ -215,7 +284,7 @@ def main():
     input_phase_ms = max(0.0, ms_per_step - serial_ms)
 
     # C2 gossip batch latency: 64 sets x 128 pubkeys, one job, host -> device -> verdict
-    c2 = None
+    c1 = c2 = c3 = c5 = None
     if rank == 0 and not args.no_c2:
         g = build_segment([0], seed=SEED + 1000)
         n2, k2 = 64, ATT_K
@@ -233,6 +302,36 @@ def main():
             lat.append((time.perf_counter() - t1) * 1e3)
             assert jr2.tolist() == [1]
         c2 = {"p50": round(float(np.median(lat[1:])), 3), "sets": n2, "pubkeys_per_set": k2}
+        # C3: one block = 128 attestation aggregates (k=128) + sync (k=512) + 2 singles, one job
+        c3a = build_segment([0], seed=SEED + 2000, att_per_block=128)
+        s3 = np.zeros((c3a["n_sets"], 192), np.uint8)
+        d.gen_sign(c3a, s3)
+        c3a.update(sigs=s3, sig_len=np.full(c3a["n_sets"], 96, np.uint32))
+        c3 = {"p50": p50_latency(d, c3a), "sets": c3a["n_sets"], "pubkey_refs": int(c3a["pk_offsets"][-1])}
+        # C1: 128 single sets, one job
+        c1a = singles(128, SEED + 3000)
+        s1 = np.zeros((128, 192), np.uint8)
+        d.gen_sign(c1a, s1)
+        c1a.update(sigs=s1, sig_len=np.full(128, 96, np.uint32))
+        c1 = {"p50": p50_latency(d, c1a), "sets": 128}
+        # C5: the C4 segment with 1% faults; the batch check fails, so every block
+        # takes the per-job final exponentiation (worker retry, multithread/worker.ts:74-85)
+        c5a, c5_expect = inject_faults(d, arrays, 0.01, SEED + 4000)
+        c5d = to_device(c5a, torch, dev)
+        c5d["scalars"] = None
+        jr5, _ = d.verify(c5d, on_device=True, want_set_codes=False)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        reps5, ok5 = 3, bool((jr5.astype(np.int32) == c5_expect).all())
+        for _ in range(reps5):
+            jr5, _ = d.verify(c5d, on_device=True, want_set_codes=False)
+            ok5 &= bool((jr5.astype(np.int32) == c5_expect).all())
+        torch.cuda.synchronize()
+        t5 = (time.perf_counter() - t1) / reps5
+        c5 = {"sets_per_s": round(c5a["n_sets"] / t5, 1), "ms_per_step": round(t5 * 1e3, 3), "fault_rate": 0.01,
+              "faulted_sets": int(max(4, int(c5a["n_sets"] * 0.01))), "jobs_true": int((c5_expect == 1).sum()),
+              "jobs_false": int((c5_expect == 0).sum()), "jobs_rejected": int((c5_expect < 0).sum()),
+              "verdicts_match_expected": ok5, "batch_retries": int(d.last_stats.batch_retries)}
     # roofline of the dominant kernel (INT32 VALU): algorithmic Fp-mul / launch time
     roof = None
     counts = fpmul_counts()
@@ -280,6 +379,9 @@ def main():
                        "sets": total_sets, "pubkey_refs": int(args.blocks * (ATT_PER_BLOCK * ATT_K + SYNC_K + 2)),
                        "table_validators": N_VALIDATORS, "jobs": args.blocks, "parallelism": f"one segment per GPU x{world}, RCCL all-gather of Miller partials"},
             "c2_gossip_latency_ms": c2,
+            "c1_singles_latency_ms": c1,
+            "c3_block_latency_ms": c3,
+            "c5_faulted_c4": c5,
             "verified": all_ok,
             "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()},
             "overlapped_phase_ms": round(input_phase_ms, 3),

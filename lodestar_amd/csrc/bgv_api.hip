@@ -421,11 +421,20 @@ int bgv_verify(bgv_ctx* c, const bgv_batch* b, int32_t* job_result, int32_t* set
     stats->n_sets = d.n_sets;
     stats->n_jobs = d.n_jobs;
     uint32_t valid_jobs = 0, valid_sets = 0;
-    if (!b->on_device) {
-      for (uint32_t j = 0; j < d.n_jobs; j++)
-        if (job_result[j] >= 0) { valid_jobs++; valid_sets += b->job_offsets[j + 1] - b->job_offsets[j]; }
-      stats->pubkeys_aggregated = b->pk_offsets[d.n_sets];
+    const uint32_t* jo = b->job_offsets;
+    std::vector<uint32_t> jo_host;
+    uint32_t pk_total = 0;
+    if (b->on_device) {  // offsets live in HBM: read them back (4 B per job)
+      jo_host.resize(d.n_jobs + 1);
+      HIPCHK(hipMemcpy(jo_host.data(), b->job_offsets, jo_host.size() * 4, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(&pk_total, b->pk_offsets + d.n_sets, 4, hipMemcpyDeviceToHost));
+      jo = jo_host.data();
+    } else {
+      pk_total = b->pk_offsets[d.n_sets];
     }
+    for (uint32_t j = 0; j < d.n_jobs; j++)
+      if (job_result[j] >= 0) { valid_jobs++; valid_sets += jo[j + 1] - jo[j]; }
+    stats->pubkeys_aggregated = pk_total;
     stats->batch_retries = (valid_jobs && !flag) ? 1u : 0u;
     stats->batch_sigs_success = flag ? valid_sets : 0u;
   }
