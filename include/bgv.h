@@ -147,6 +147,15 @@ int bgv_pubkeys_count(bgv_ctx* ctx, uint32_t* count);
 /* read back entries as 96-byte uncompressed big-endian (tests, checkpoints) */
 int bgv_pubkeys_get(bgv_ctx* ctx, uint32_t first_index, uint32_t n, uint8_t* out96);
 
+/* Untrusted-key validation: bls.PublicKey.fromBytes(pk, CoordType.affine,
+ * validate=true) for n 48-byte compressed keys, as deposits do once per new
+ * validator (state-transition/src/block/processDeposit.ts:57-66; also
+ * beacon-node/src/chain/validation/blobsSidecar.ts:129).  codes[i] is a
+ * bgv_set_code: 0 valid, BAD_ENCODING (flags / x >= p), POINT_NOT_ON_CURVE,
+ * PK_IS_INFINITY, POINT_NOT_IN_GROUP ([r]P != O).  Valid keys can then be
+ * appended with bgv_pubkeys_set.                                          */
+int bgv_pubkeys_validate(bgv_ctx* ctx, const uint8_t* pk48, uint32_t n, int32_t* codes);
+
 /* Verify one device batch.  Replaces the worker body
  * verifyManySignatureSets (multithread/worker.ts:30-106) together with
  * verifySignatureSetsMaybeBatch (maybeBatch.ts:16-38) and the main-thread

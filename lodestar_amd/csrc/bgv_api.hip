@@ -229,6 +229,20 @@ int bgv_pubkeys_get(bgv_ctx* c, uint32_t first, uint32_t n, uint8_t* out96) {
   return BGV_OK;
 }
 
+int bgv_pubkeys_validate(bgv_ctx* c, const uint8_t* pk48, uint32_t n, int32_t* codes) {
+  if (!c || (n && (!pk48 || !codes))) return fail(BGV_E_INVALID_ARG, "null argument");
+  if (n == 0) return BGV_OK;
+  HIPCHK(hipSetDevice(c->device));
+  if (int r = c->raw_in.ensure((size_t)n * 48)) return r;
+  if (int r = c->sig_code.ensure(n)) return r;
+  HIPCHK(hipMemcpyAsync(c->raw_in.p, pk48, (size_t)n * 48, hipMemcpyHostToDevice, c->st));
+  launch_pk_validate(c->st, c->raw_in.p, n, c->sig_code.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(codes, c->sig_code.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return BGV_OK;
+}
+
 // ---------------------------------------------------------------- batches
 
 static void random_scalars(uint64_t* s, uint32_t n) {

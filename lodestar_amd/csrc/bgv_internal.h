@@ -78,6 +78,7 @@ void launch_raw_pks(hipStream_t st, const uint8_t* raw, g1a* out, uint32_t n);
 void launch_table_from_compressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n);
 void launch_table_from_uncompressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n);
 void launch_table_export(hipStream_t st, const g1a* tab, uint8_t* out, uint32_t n);
+void launch_pk_validate(hipStream_t st, const uint8_t* in, uint32_t n, int32_t* codes);
 void launch_prep(hipStream_t st, const dev_batch& b, const dev_work& w);  // before ST_PK / ST_MILLER
 void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work& w);
 void launch_fp12_tail(hipStream_t st, int stage, const dev_batch& b, const dev_work& w);  // bgv_tail.hip

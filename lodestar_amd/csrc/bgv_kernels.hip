@@ -519,6 +519,28 @@ BGV_NI void jac_mul_u256(jac_t<F>& r, const jac_t<F>& p, const uint32_t k[8]) {
   r = acc;
 }
 
+// PublicKey.fromBytes(pk, affine, validate=true) for untrusted keys
+// (processDeposit.ts:59): decode + on-curve, infinity -> BLST_PK_IS_INFINITY,
+// then the definitional subgroup test [r]P = O (once per deposit, so the
+// 255 doublings are not worth an endomorphism shortcut)
+__global__ void BGV_BULK k_pk_validate(const uint8_t* in, uint32_t n, int32_t* codes) {
+  const uint32_t t = gtid();
+  if (t >= n) return;
+  g1a a;
+  bool inf = false;
+  int32_t c = g1_decompress(a, inf, in + 48u * t);
+  if (c == C_OK && inf) c = C_PK_IS_INFINITY;
+  if (c == C_OK) {
+    g1j p, q;
+    p.x = a.x;
+    p.y = a.y;
+    fe_one(p.z);
+    jac_mul_u256(q, p, FR_R);
+    if (!jac_is_inf(q)) c = C_POINT_NOT_IN_GROUP;
+  }
+  codes[t] = c;
+}
+
 // sk_i = SHA256("bgv-sk" || LE64(seed) || LE32(i)) (big-endian integer) mod r
 __device__ void gen_sk(uint32_t sk[8], uint64_t seed, uint32_t i) {
   uint32_t blk[16];
@@ -629,6 +651,9 @@ void launch_table_from_compressed(hipStream_t st, const uint8_t* in, g1a* out, u
 }
 void launch_table_from_uncompressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n) {
   BGV_LAUNCH(k_table_from_uncompressed, n, in, out, n);
+}
+void launch_pk_validate(hipStream_t st, const uint8_t* in, uint32_t n, int32_t* codes) {
+  BGV_LAUNCH(k_pk_validate, n, in, n, codes);
 }
 void launch_table_export(hipStream_t st, const g1a* tab, uint8_t* out, uint32_t n) {
   BGV_LAUNCH(k_table_export, n, tab, out, n);

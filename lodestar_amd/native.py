@@ -44,7 +44,7 @@ N_STAGES = 12
 
 EXPORTS = [
     "bgv_abi_version", "bgv_set_code_name", "bgv_stage_name", "bgv_last_error", "bgv_open", "bgv_close",
-    "bgv_pubkeys_set", "bgv_pubkeys_count", "bgv_pubkeys_get", "bgv_verify", "bgv_partial",
+    "bgv_pubkeys_set", "bgv_pubkeys_count", "bgv_pubkeys_get", "bgv_pubkeys_validate", "bgv_verify", "bgv_partial",
     "bgv_combine_final", "bgv_gen_keys", "bgv_gen_sign", "bgv_bench_fpmul", "bgv_bench_mad",
 ]
 
@@ -121,6 +121,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
             "bgv_pubkeys_set": ([P, u32, u32, P, u32], ctypes.c_int),
             "bgv_pubkeys_count": ([P, ctypes.POINTER(u32)], ctypes.c_int),
             "bgv_pubkeys_get": ([P, u32, u32, P], ctypes.c_int),
+            "bgv_pubkeys_validate": ([P, P, u32, P], ctypes.c_int),
             "bgv_verify": ([P, ctypes.POINTER(BgvBatch), P, P, ctypes.POINTER(BgvStats)], ctypes.c_int),
             "bgv_partial": ([P, ctypes.POINTER(BgvBatch), P, P, ctypes.POINTER(i32)], ctypes.c_int),
             "bgv_combine_final": ([P, P, u32, ctypes.POINTER(i32)], ctypes.c_int),
@@ -192,6 +193,15 @@ class Device:
         out = np.zeros(n * 96, dtype=np.uint8)
         self._check(self.lib.bgv_pubkeys_get(self.h, first, n, out.ctypes.data))
         return out.tobytes()
+
+    def pubkeys_validate(self, pk48: bytes) -> np.ndarray:
+        """PublicKey.fromBytes(pk, affine, validate=true) for each 48-byte key
+        (processDeposit.ts:59): per-key bgv_set_code (0 = valid)."""
+        n = len(pk48) // 48
+        buf = np.frombuffer(pk48, dtype=np.uint8).copy()
+        codes = np.zeros(max(n, 1), dtype=np.int32)
+        self._check(self.lib.bgv_pubkeys_validate(self.h, buf.ctypes.data, n, codes.ctypes.data))
+        return codes[:n]
 
     def gen_keys(self, first: int, n: int, seed: int):
         self._check(self.lib.bgv_gen_keys(self.h, first, n, seed))

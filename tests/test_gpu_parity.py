@@ -227,3 +227,45 @@ def _synthetic_on(dev_, n_sets, k, first, n_keys, seed, fault_every=0):
     arrays.update(sigs=sigs, sig_len=np.full(n_sets, 96, np.uint32),
                   scalars=rng.integers(1, 2**63, size=n_sets, dtype=np.uint64))
     return arrays, bad
+
+
+def _oracle_pk_code(b: bytes) -> int:
+    """PublicKey.fromBytes(b, affine, validate=true) per the oracle: decode
+    code, then infinity -> 6 (BLST_PK_IS_INFINITY), [r]P != O -> 3."""
+    code, pt = B.g1_decompress(b)
+    if code:
+        return code
+    if pt is None:
+        return 6
+    return 0 if B.g1_in_subgroup(pt) else 3
+
+
+def test_pubkey_validation_matches_oracle(dev):
+    """bgv_pubkeys_validate == the oracle on the 100 interop keys, their
+    negations, and every rejection class (processDeposit.ts:57-66)."""
+    pks = G.interop_pubkeys48()
+    keys = [pks[48 * i : 48 * i + 48] for i in range(100)]
+    keys += [bytes([k[0] ^ 0x20]) + k[1:] for k in keys[:4]]           # -P: still in G1
+    keys.append(bytes([0xC0]) + bytes(47))                               # infinity
+    keys.append(bytes([keys[0][0] & 0x7F]) + keys[0][1:])                # compression flag cleared
+    keys.append(bytes([0xE0]) + bytes(47))                               # infinity flag with sign bit
+    pb = bytearray(B.P.to_bytes(48, "big"))
+    pb[0] |= 0x80
+    keys.append(bytes(pb))                                               # x = p
+    rng = np.random.default_rng(17)
+    off_curve = in_e1_not_g1 = 0
+    while off_curve < 3 or in_e1_not_g1 < 3:
+        x = int.from_bytes(rng.bytes(48), "big") % B.P
+        y = B.fp_sqrt((x * x * x + B.B1) % B.P)
+        if y is None and off_curve < 3:
+            xb = bytearray(x.to_bytes(48, "big"))
+            xb[0] |= 0x80
+            keys.append(bytes(xb))
+            off_curve += 1
+        elif y is not None and in_e1_not_g1 < 3 and not B.g1_in_subgroup((x, y)):
+            keys.append(B.g1_compress((x, y)))
+            in_e1_not_g1 += 1
+    got = dev.pubkeys_validate(b"".join(keys)).tolist()
+    want = [_oracle_pk_code(k) for k in keys]
+    assert got == want
+    assert set(want) == {0, 1, 2, 3, 6}
