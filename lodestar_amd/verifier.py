@@ -309,6 +309,28 @@ class BlsGpuVerifier:
             raise r
         return r
 
+    def verify_signature_set(self, s: ISignatureSet) -> bool:
+        """util/signatureSets.ts:24-38 verifySignatureSet: the signature is
+        parsed and group-checked; single -> verify(pk, root), aggregate ->
+        verifyAggregate(pks, root).  One set, one device batch (n = 1): the
+        random scalar of the batch equation cannot change the verdict (GT has
+        prime order r and the scalar is nonzero mod r)."""
+        if s.type == SignatureSetType.aggregate and len(s.pubkeys) == 0:
+            raise BlsError("EMPTY_AGGREGATE_ARRAY")
+        return self.verify_signature_sets_maybe_batch([s])
+
+    def is_valid_bls_aggregate(self, public_keys: list[PublicKey], message: bytes, signature: bytes) -> bool:
+        """light-client/src/validation.ts:152-175 isValidBlsAggregate: aggregate
+        the keys, deserialize + group-check the signature, verify; each failure
+        re-thrown with the reference's prefix."""
+        if len(public_keys) == 0:
+            raise BlsError("Error aggregating pubkeys: EMPTY_AGGREGATE_ARRAY")
+        s = create_aggregate_signature_set_from_components(list(public_keys), message, signature)
+        try:
+            return self.verify_signature_sets_maybe_batch([s])
+        except BlsError as e:
+            raise BlsError(f"Error deserializing signature: {e}", getattr(e, "code", None)) from e
+
     # -- queueing -------------------------------------------------------------
     async def _queue_work(self, sets, opts) -> bool:
         if self._closed:

@@ -269,3 +269,32 @@ def test_pubkey_validation_matches_oracle(dev):
     want = [_oracle_pk_code(k) for k in keys]
     assert got == want
     assert set(want) == {0, 1, 2, 3, 6}
+
+
+def test_single_set_and_light_client_aggregate():
+    """verifySignatureSet (util/signatureSets.ts:24-38) and the light client's
+    isValidBlsAggregate (light-client/src/validation.ts:152-175) on the device,
+    with oracle-made keys and signatures (sk = 0x0101.., 0x0202.., 0x0303..)."""
+    from lodestar_amd import verifier as V
+    sks = [int.from_bytes(bytes([k]) * 32, "big") % B.R for k in (1, 2, 3)]
+    pks = [V.PublicKey.from_bytes(B.g1_serialize(B.sk_to_pk(sk))) for sk in sks]
+    msg = bytes(range(32))
+    agg_sig = B.g2_compress(B.sign(sum(sks) % B.R, msg))
+    one_sig = B.g2_compress(B.sign(sks[0], msg))
+    pool = V.BlsGpuVerifier(devices=(0,))
+    try:
+        assert pool.is_valid_bls_aggregate(pks, msg, agg_sig)
+        assert not pool.is_valid_bls_aggregate(pks[:2], msg, agg_sig)
+        assert not pool.is_valid_bls_aggregate(pks, bytes(32), agg_sig)
+        with pytest.raises(V.BlsError, match="Error aggregating pubkeys"):
+            pool.is_valid_bls_aggregate([], msg, agg_sig)
+        with pytest.raises(V.BlsError, match="Error deserializing signature: BLST_ERROR: BLST_INVALID_SIZE"):
+            pool.is_valid_bls_aggregate(pks, msg, agg_sig[:32])
+        single = V.create_single_signature_set_from_components
+        aggregate = V.create_aggregate_signature_set_from_components
+        assert pool.verify_signature_set(single(pks[0], msg, one_sig))
+        assert not pool.verify_signature_set(single(pks[1], msg, one_sig))
+        assert pool.verify_signature_set(aggregate(pks, msg, agg_sig))
+        assert not pool.verify_signature_set(aggregate(pks[1:], msg, agg_sig))
+    finally:
+        asyncio.run(pool.close())
