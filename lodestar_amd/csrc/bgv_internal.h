@@ -19,6 +19,7 @@ struct dev_batch {
   uint32_t chunk_bound;  // upper bound of pubkey chunks (grid of k_pk_chunk)
   uint32_t miller_coop;     // 1: six-lane cooperative Miller loop (miller_coop.h)
   uint32_t pairs_per_item;  // Miller pairs sharing one accumulator (1, or 2 for batches that fill the GPU)
+  uint32_t msm;             // 1: per-job bucket MSM for sum r_i sigma_i (k_msm_*), 0: per-set [r_i] sigma_i + tree
   const uint32_t* job_off;
   const uint32_t* pk_off;
   const uint32_t* pk_idx;
@@ -36,6 +37,9 @@ struct dev_work {
   uint32_t* sig_inf;  // signature is the identity
   int32_t* sig_code;  // parse / subgroup outcome
   g2a* h_aff;         // H(m)
+  g2j* msm_bucket;    // [n_jobs * 16 windows * 15 buckets] (msm mode)
+  uint32_t* msm_mask; // [n_jobs * 16] occupied buckets of each (job, window)
+  g2j* msm_win;       // [n_jobs * 16] window sums
   uint32_t* chunk_off;  // [n_sets + 1] scan of per-set pubkey chunk counts
   uint32_t* chunk_set;  // set of every chunk
   g1j* pk_part;         // per-chunk partial sums

@@ -298,3 +298,33 @@ def test_single_set_and_light_client_aggregate():
         assert not pool.verify_signature_set(aggregate(pks[1:], msg, agg_sig))
     finally:
         asyncio.run(pool.close())
+
+
+def test_signature_msm_bit_identical_to_per_set_scaling(monkeypatch):
+    """sum_j r_i sigma_i by the per-job bucket MSM (k_msm_*, default for
+    large batches) and by per-set [r_i] sigma_i + tree give the same S_job:
+    the batch partial (which holds the (-G1, S_job) Miller values) is
+    byte-identical, and the golden verdicts hold in both modes."""
+    from lodestar_amd import native
+    outs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("BGV_MSM", mode)
+        d = native.Device(0)
+        try:
+            d.pubkeys_set(0, G.interop_pubkeys48(), native.PK_COMPRESSED_48)
+            a, _, _ = G.golden_arrays([0, 1, 9, 10, 11, 12, 13], scalars_seed=5)
+            part, _, ok = d.partial(a)
+            arrays, expected, codes = G.golden_arrays(scalars_seed=5)
+            jr, sc = d.verify(arrays)
+            assert jr.tolist() == expected and sc.tolist() == codes
+            d.gen_keys(1000, 256, 5)
+            syn, bad = _synthetic_on(d, 300, 8, 1000, 256, 4, fault_every=23)
+            syn["n_jobs"] = 3
+            syn["job_offsets"] = np.array([0, 100, 200, 300], np.uint32)
+            syn_part, _, _ = d.partial(syn)
+            jr2, _ = d.verify(syn)
+            assert jr2.tolist() == [int(not bad[i * 100:(i + 1) * 100].any()) for i in range(3)]
+            outs[mode] = (part, ok, syn_part)
+        finally:
+            d.close()
+    assert outs["0"] == outs["1"]
