@@ -472,10 +472,50 @@ BGV_NI void fp_inv(fp_t& r, const fp_t& a) {
   fp_mul(r, x, R3_MOD);
 }
 
+// r = a^e for a fixed exponent given as a 4-bit sliding-window plan
+// (tools/gen_constants.py pow_plan): odd powers a, a^3, ..., a^15, then per
+// step `shift` squarings and one product by a table entry.  The plan is the
+// same for every lane, so the table entry is chosen by a scalar branch and
+// the table stays in registers.  (p+1)/4: 378 squarings + 86 products
+// (+8 for the table) against 378 + 228 for plain binary.
+BGV_NI void fp_pow_plan(fp_t& r, const fp_t& a, const uint8_t* shift, const uint8_t* idx, uint32_t n, uint32_t first) {
+  fp_t t[8], a2;
+  t[0] = a;
+  fp_sqr(a2, a);
+#pragma unroll
+  for (int k = 1; k < 8; k++) fp_mul(t[k], t[k - 1], a2);
+  fp_t acc = t[0];
+#pragma unroll
+  for (int k = 1; k < 8; k++)
+    if (first == (uint32_t)k) acc = t[k];
+  for (uint32_t s = 0; s < n; s++) {
+    const uint32_t sh = shift[s];
+    for (uint32_t k = 0; k < sh; k++) fp_sqr(acc, acc);
+    switch (idx[s]) {
+      case 0: fp_mul(acc, acc, t[0]); break;
+      case 1: fp_mul(acc, acc, t[1]); break;
+      case 2: fp_mul(acc, acc, t[2]); break;
+      case 3: fp_mul(acc, acc, t[3]); break;
+      case 4: fp_mul(acc, acc, t[4]); break;
+      case 5: fp_mul(acc, acc, t[5]); break;
+      case 6: fp_mul(acc, acc, t[6]); break;
+      case 7: fp_mul(acc, acc, t[7]); break;
+      default: break;
+    }
+  }
+  r = acc;
+}
+
+// a^((p+1)/4) and a^((p-3)/4)
+BGV_HD void fp_pow_sqrt(fp_t& r, const fp_t& a) { fp_pow_plan(r, a, POWP_SQRT_SHIFT, POWP_SQRT_IDX, POWP_SQRT_N, POWP_SQRT_FIRST); }
+BGV_HD void fp_pow_sqrt_tail(fp_t& r, const fp_t& a) {
+  fp_pow_plan(r, a, POWP_SQRT_TAIL_SHIFT, POWP_SQRT_TAIL_IDX, POWP_SQRT_TAIL_N, POWP_SQRT_TAIL_FIRST);
+}
+
 // candidate square root a^((p+1)/4); returns true iff it squares back to a
 BGV_HD bool fp_sqrt(fp_t& r, const fp_t& a) {
   fp_t s, chk;
-  fp_pow(s, a, EXP_P_PLUS_1_DIV_4);
+  fp_pow_sqrt(s, a);
   fp_sqr(chk, s);
   r = s;
   return fp_eq(chk, a);

@@ -115,7 +115,7 @@ BGV_NI void fp2_sqrt_tail(fp2_t& r, const fp2_t& a, const fp_t& d) {
   fp_t t, s, st, s2t, as;
   fp_add(t, a.c0, d);
   fp_half(t, t);
-  fp_pow(s, t, EXP_P_MINUS_3_DIV_4);
+  fp_pow_sqrt_tail(s, t);
   fp_mul(st, s, t);
   fp_mul(s2t, st, s);
   fp_mul(as, a.c1, s);

@@ -176,7 +176,7 @@ BGV_NI void map_to_curve_sswu(g2a& out, const fp2_t& u) {
   // (RFC 9380 6.6.2 computes is_square(gx1) and sqrt() separately: 4 exponentiations.)
   fp_t n1, d, chk, nu, nu3, d2;
   fp2_norm(n1, gx1);
-  fp_pow(d, n1, EXP_P_PLUS_1_DIV_4);
+  fp_pow_sqrt(d, n1);
   fp_sqr(chk, d);
   const bool sq = fp_eq(chk, n1);
   fp2_norm(nu, u);

@@ -192,6 +192,47 @@ w("")
 w("// exponents (plain integers, 12 x u32) for Fermat inverse / sqrt / Legendre")
 w("BGV_CONST fp_t EXP_P_MINUS_2 = " + fp_lit(P - 2, False) + ";")
 w("BGV_CONST fp_t EXP_P_PLUS_1_DIV_4 = " + fp_lit((P + 1) // 4, False) + ";")
+
+
+def pow_plan(e, wbits=4):
+    """4-bit sliding-window plan of a fixed exponent, MSB first: the first
+    window's odd value selects the start, then each step squares `shift`
+    times and multiplies by a^(2 idx + 1) (idx 0xFF: squarings only)."""
+    b = bin(e)[2:]
+    i, first, pend, steps = 0, None, 0, []
+    while i < len(b):
+        if b[i] == "0":
+            pend += 1
+            i += 1
+            continue
+        j = min(i + wbits, len(b))
+        while b[j - 1] == "0":
+            j -= 1
+        v = int(b[i:j], 2)
+        if first is None:
+            first = (v - 1) // 2
+        else:
+            steps.append((pend + (j - i), (v - 1) // 2))
+        pend = 0
+        i = j
+    if pend:
+        steps.append((pend, 0xFF))
+    acc = 2 * first + 1  # check the plan reproduces e
+    for sh, ix in steps:
+        acc <<= sh
+        if ix != 0xFF:
+            acc += 2 * ix + 1
+    assert acc == e
+    return first, steps
+
+
+for _name, _e in (("SQRT", (P + 1) // 4), ("SQRT_TAIL", (P - 3) // 4)):
+    _first, _steps = pow_plan(_e)
+    w("// sliding-window plan of %s (fp.h fp_pow_plan): %d steps, %d products" % (
+        "(p+1)/4" if _name == "SQRT" else "(p-3)/4", len(_steps), sum(1 for _s in _steps if _s[1] != 0xFF)))
+    w("constexpr uint32_t POWP_%s_N = %d, POWP_%s_FIRST = %d;" % (_name, len(_steps), _name, _first))
+    w("BGV_CONST uint8_t POWP_%s_SHIFT[%d] = {%s};" % (_name, len(_steps), ", ".join(str(a) for a, _ in _steps)))
+    w("BGV_CONST uint8_t POWP_%s_IDX[%d] = {%s};" % (_name, len(_steps), ", ".join(str(b_) for _, b_ in _steps)))
 w("BGV_CONST fp_t EXP_P_MINUS_3_DIV_4 = " + fp_lit((P - 3) // 4, False) + ";")
 w("BGV_CONST fp_t EXP_P_MINUS_1_DIV_2 = " + fp_lit((P - 1) // 2, False) + ";")
 w("// (p - 1) / 2 plain, for the lexicographic sign of a coordinate")
