@@ -790,12 +790,11 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       BGV_LAUNCH(k_miller, b.n_sets / b.pairs_per_item + b.n_jobs, b, w, 0u);  // >= items (launch_prep)
       break;
     case ST_MILLER_JOBS:  // (-G1, S_job) pairs: needs ST_S_TREE
-      if (b.miller_coop) {
-        if (b.n_jobs)
-          hipLaunchKernelGGL(k_miller_coop, dim3((b.n_jobs + COOP_GROUPS - 1) / COOP_GROUPS), dim3(64), 0, st, b, w, b.n_sets, b.n_jobs);
-        break;
-      }
-      BGV_LAUNCH(k_miller, b.n_jobs, b, w, 1u);
+      // always the six-lane loop: one pair per job is latency-bound (a lone
+      // lane takes ~19 ms at C4, the cooperative loop ~5 ms) and its waves
+      // fit on the SIMDs the set-pair kernel leaves free
+      if (b.n_jobs)
+        hipLaunchKernelGGL(k_miller_coop, dim3((b.n_jobs + COOP_GROUPS - 1) / COOP_GROUPS), dim3(64), 0, st, b, w, b.n_sets, b.n_jobs);
       break;
     case ST_F_TREE:
       launch_fp12_tail(st, stage, b, w);  // bgv_tail.hip
