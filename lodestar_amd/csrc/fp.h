@@ -44,6 +44,13 @@ BGV_HD void fp_select(fp_t& r, bool c, const fp_t& a, const fp_t& b) {
 }
 
 // r = a - p if a >= p  (a < 2p)
+#ifndef BGV_FPMUL28
+#define BGV_FPMUL28 1
+#endif
+#ifndef BGV_FPMUL28_LAZY
+#define BGV_FPMUL28_LAZY BGV_FPMUL28
+#endif
+
 BGV_HD void fp_reduce_once(fp_t& r, const fp_t& a) {
   uint32_t t[NL];
   uint32_t borrow = 0;
@@ -73,6 +80,26 @@ BGV_HD void fp_add(fp_t& r, const fp_t& a, const fp_t& b) {
 }
 
 BGV_HD void fp_dbl(fp_t& r, const fp_t& a) { fp_add(r, a, a); }
+
+// Lazy forms, ONLY for operands that go straight into fp_mul: the result is
+// < 2p < 2^382 (not reduced).  fp_mul28 accepts inputs < 2^382 (the 8-bit
+// pre-shift still fits its 14 x 28-bit digits) and, with both inputs < 2p,
+// its Montgomery sum stays below 4p^2 2^8 / 2^392 + p < 1.41 p before the
+// final subtraction, so its output is canonical.  The 32-bit CIOS variant
+// (BGV_FPMUL28=0) keeps the reduced forms.
+BGV_HD void fp_add_lazy(fp_t& r, const fp_t& a, const fp_t& b) {
+#if BGV_FPMUL28_LAZY
+  uint32_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    const uint64_t t = (uint64_t)a.l[i] + b.l[i] + carry;
+    r.l[i] = (uint32_t)t;
+    carry = (uint32_t)(t >> 32);
+  }
+#else
+  fp_add(r, a, b);
+#endif
+}
 
 BGV_HD void fp_sub(fp_t& r, const fp_t& a, const fp_t& b) {
   uint32_t t[NL];

@@ -41,8 +41,8 @@ __device__ void c_mul(wfp12* out, const wfp12* a, const wfp12* b, cscratch* s) {
       u = x.c1;
       v = y.c1;
     } else {
-      fp_add(u, x.c0, x.c1);
-      fp_add(v, y.c0, y.c1);
+      fp_add_lazy(u, x.c0, x.c1);  // < 2p, product inputs only
+      fp_add_lazy(v, y.c0, y.c1);
     }
     fp_mul(s->p[l], u, v);
   }

@@ -30,8 +30,8 @@ BGV_NI2 void fp2_mul(fp2_t& r, const fp2_t& a, const fp2_t& b) {
   fp_t t0, t1, t2, t3;
   fp_mul(t0, a.c0, b.c0);
   fp_mul(t1, a.c1, b.c1);
-  fp_add(t2, a.c0, a.c1);
-  fp_add(t3, b.c0, b.c1);
+  fp_add_lazy(t2, a.c0, a.c1);  // < 2p, product inputs only
+  fp_add_lazy(t3, b.c0, b.c1);
   fp_mul(t2, t2, t3);
   fp_sub(r.c0, t0, t1);
   fp_sub(t2, t2, t0);
@@ -44,8 +44,8 @@ BGV_HD void fp2_mul_inl(fp2_t& r, const fp2_t& a, const fp2_t& b) {
   fp_t t0, t1, t2, t3;
   fp_mul(t0, a.c0, b.c0);
   fp_mul(t1, a.c1, b.c1);
-  fp_add(t2, a.c0, a.c1);
-  fp_add(t3, b.c0, b.c1);
+  fp_add_lazy(t2, a.c0, a.c1);  // < 2p, product inputs only
+  fp_add_lazy(t3, b.c0, b.c1);
   fp_mul(t2, t2, t3);
   fp_sub(r.c0, t0, t1);
   fp_sub(t2, t2, t0);
@@ -55,7 +55,7 @@ BGV_HD void fp2_mul_inl(fp2_t& r, const fp2_t& a, const fp2_t& b) {
 // complex squaring: 2 Fp products
 BGV_NI2 void fp2_sqr(fp2_t& r, const fp2_t& a) {
   fp_t t0, t1, t2;
-  fp_add(t0, a.c0, a.c1);
+  fp_add_lazy(t0, a.c0, a.c1);  // < 2p, product input only
   fp_sub(t1, a.c0, a.c1);
   fp_mul(t2, a.c0, a.c1);
   fp_mul(r.c0, t0, t1);

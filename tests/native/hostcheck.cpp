@@ -38,6 +38,35 @@ void hc_fp_inv(const uint8_t* a, uint8_t* out) { fp_t x, z; get_fp(x, a); fp_inv
 void hc_fp2_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { fp2_t x, y, z; get_fp2(x, a); get_fp2(y, b); fp2_mul(z, x, y); put_fp2(out, z); }
 void hc_fp2_sqr(const uint8_t* a, uint8_t* out) { fp2_t x, z; get_fp2(x, a); fp2_sqr(z, x); put_fp2(out, z); }
 void hc_fp2_inv(const uint8_t* a, uint8_t* out) { fp2_t x, z; get_fp2(x, a); fp2_inv(z, x); put_fp2(out, z); }
+// fp_mul on unreduced inputs a + p, b + p (< 2p, the fp_add_lazy range) must
+// return the same canonical limbs as on a, b; returns the number of failures
+int hc_lazy_mul_canonical(uint64_t seed, int n) {
+  uint64_t x = seed | 1;
+  auto rnd = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+  int bad = 0;
+  for (int it = 0; it < n; it++) {
+    fp_t a, b;
+    for (int i = 0; i < NL; i++) { a.l[i] = (uint32_t)rnd(); b.l[i] = (uint32_t)rnd(); }
+    a.l[NL - 1] &= 0x1fffffffu; b.l[NL - 1] &= 0x1fffffffu;
+    if (it < 3) { a = P_MOD; a.l[0] -= 1 + it; }  // p-1, p-2, p-3
+    fp_reduce_once(a, a); fp_reduce_once(a, a); fp_reduce_once(b, b); fp_reduce_once(b, b);
+    if (!fp_plain_lt_p(a)) fp_sub(a, a, P_MOD);
+    if (!fp_plain_lt_p(b)) fp_sub(b, b, P_MOD);
+    fp_t ap, bp, r1, r2, r3;
+    uint64_t c = 0, d = 0;
+    for (int i = 0; i < NL; i++) {
+      c += (uint64_t)a.l[i] + P_MOD.l[i]; ap.l[i] = (uint32_t)c; c >>= 32;
+      d += (uint64_t)b.l[i] + P_MOD.l[i]; bp.l[i] = (uint32_t)d; d >>= 32;
+    }
+    fp_mul(r1, ap, bp);
+    fp_mul(r2, a, b);
+    fp_mul(r3, ap, b);
+    for (int i = 0; i < NL; i++) if (r1.l[i] != r2.l[i] || r3.l[i] != r2.l[i]) { bad++; break; }
+    if (!fp_plain_lt_p(r1)) bad++;
+  }
+  return bad;
+}
+
 int hc_fp2_sqrt(const uint8_t* a, uint8_t* out) { fp2_t x, z; get_fp2(x, a); int ok = fp2_sqrt(z, x); put_fp2(out, z); return ok; }
 int hc_fp2_is_square(const uint8_t* a) { fp2_t x; get_fp2(x, a); return fp2_is_square(x); }
 int hc_fp2_sgn0(const uint8_t* a) { fp2_t x; get_fp2(x, a); return (int)fp2_sgn0(x); }

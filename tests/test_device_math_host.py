@@ -4,6 +4,7 @@ every algebraic layer the HIP kernels are built from (field tower, curve
 formulas, decompression, subgroup test, hash_to_G2 stages, Miller loop steps,
 final exponentiation) on the CPU; tests/test_gpu_*.py then check that the
 kernels built from the same headers agree on the GPU."""
+import ctypes
 import random
 
 import pytest
@@ -65,6 +66,18 @@ def test_fp2_ops():
         lib.hc_fp2_inv(H.fp2_b(a), o)
         assert B.f2_eq(B.f2_mul(H.b_fp2(o.raw), a), B.F2_ONE)
         assert lib.hc_fp2_sgn0(H.fp2_b(a)) == B.f2_sgn0(a)
+    assert lib.hc_lazy_mul_canonical(ctypes.c_uint64(12345), 20000) == 0
+    # lazy Karatsuba sums (fp_add_lazy, < 2p): Montgomery images at p-1, p-2 make them largest
+    rinv = pow(2**384, -1, B.P)
+    hi = [(B.P - k) * rinv % B.P for k in (1, 2, 3)] + [B.P - 1, 1, 0, (B.P - 1) // 2 * rinv % B.P]
+    for x0 in hi:
+        for x1 in hi:
+            a, b = (x0, x1), (x1, hi[0])
+            o = H.buf(96)
+            lib.hc_fp2_mul(H.fp2_b(a), H.fp2_b(b), o)
+            assert H.b_fp2(o.raw) == B.f2_mul(a, b)
+            lib.hc_fp2_sqr(H.fp2_b(a), o)
+            assert H.b_fp2(o.raw) == B.f2_sqr(a)
     for _ in range(40):
         a = rfp2()
         sq = B.f2_is_square(a)
