@@ -51,15 +51,40 @@ BGV_HD void fp_select(fp_t& r, bool c, const fp_t& a, const fp_t& b) {
 #define BGV_FPMUL28_LAZY BGV_FPMUL28
 #endif
 
+// 32-bit carry / borrow steps.  Under clang they are the add/sub-with-carry
+// builtins, so a 12-limb chain is v_add_co/v_addc_co (v_sub_co/v_subb_co)
+// on gfx950; the 64-bit "d >> 63" form compiled to sign extensions plus a
+// hazard NOP per limb.  g++ (host tests) takes the portable form.
+BGV_HD uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t& cout) {
+#if defined(__clang__)
+  unsigned int co;
+  const uint32_t s = __builtin_addc(a, b, cin, &co);
+  cout = co;
+  return s;
+#else
+  const uint64_t t = (uint64_t)a + b + cin;
+  cout = (uint32_t)(t >> 32);
+  return (uint32_t)t;
+#endif
+}
+BGV_HD uint32_t subb32(uint32_t a, uint32_t b, uint32_t bin, uint32_t& bout) {
+#if defined(__clang__)
+  unsigned int bo;
+  const uint32_t d = __builtin_subc(a, b, bin, &bo);
+  bout = bo;
+  return d;
+#else
+  const uint64_t d = (uint64_t)a - b - bin;
+  bout = (uint32_t)(d >> 63);
+  return (uint32_t)d;
+#endif
+}
+
 BGV_HD void fp_reduce_once(fp_t& r, const fp_t& a) {
   uint32_t t[NL];
   uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < NL; i++) {
-    uint64_t d = (uint64_t)a.l[i] - P_MOD.l[i] - borrow;
-    t[i] = (uint32_t)d;
-    borrow = (uint32_t)(d >> 63);
-  }
+  for (int i = 0; i < NL; i++) t[i] = subb32(a.l[i], P_MOD.l[i], borrow, borrow);
   // borrow == 1  <=>  a < p  -> keep a
   const uint32_t m = 0u - borrow;
 #pragma unroll
@@ -70,11 +95,7 @@ BGV_HD void fp_add(fp_t& r, const fp_t& a, const fp_t& b) {
   fp_t s;
   uint32_t carry = 0;
 #pragma unroll
-  for (int i = 0; i < NL; i++) {
-    uint64_t t = (uint64_t)a.l[i] + b.l[i] + carry;
-    s.l[i] = (uint32_t)t;
-    carry = (uint32_t)(t >> 32);
-  }
+  for (int i = 0; i < NL; i++) s.l[i] = addc32(a.l[i], b.l[i], carry, carry);
   // p < 2^381, so a + b < 2^382 never carries out of 12 limbs
   fp_reduce_once(r, s);
 }
@@ -91,11 +112,7 @@ BGV_HD void fp_add_lazy(fp_t& r, const fp_t& a, const fp_t& b) {
 #if BGV_FPMUL28_LAZY
   uint32_t carry = 0;
 #pragma unroll
-  for (int i = 0; i < NL; i++) {
-    const uint64_t t = (uint64_t)a.l[i] + b.l[i] + carry;
-    r.l[i] = (uint32_t)t;
-    carry = (uint32_t)(t >> 32);
-  }
+  for (int i = 0; i < NL; i++) r.l[i] = addc32(a.l[i], b.l[i], carry, carry);
 #else
   fp_add(r, a, b);
 #endif
@@ -105,20 +122,12 @@ BGV_HD void fp_sub(fp_t& r, const fp_t& a, const fp_t& b) {
   uint32_t t[NL];
   uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < NL; i++) {
-    uint64_t d = (uint64_t)a.l[i] - b.l[i] - borrow;
-    t[i] = (uint32_t)d;
-    borrow = (uint32_t)(d >> 63);
-  }
+  for (int i = 0; i < NL; i++) t[i] = subb32(a.l[i], b.l[i], borrow, borrow);
   // if a < b add p back
   const uint32_t m = 0u - borrow;
   uint32_t carry = 0;
 #pragma unroll
-  for (int i = 0; i < NL; i++) {
-    uint64_t s = (uint64_t)t[i] + (P_MOD.l[i] & m) + carry;
-    r.l[i] = (uint32_t)s;
-    carry = (uint32_t)(s >> 32);
-  }
+  for (int i = 0; i < NL; i++) r.l[i] = addc32(t[i], P_MOD.l[i] & m, carry, carry);
 }
 
 BGV_HD void fp_neg(fp_t& r, const fp_t& a) {
