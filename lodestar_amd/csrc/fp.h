@@ -572,10 +572,7 @@ BGV_HD void fp_from_mont(fp_t& r, const fp_t& a) {
 BGV_HD bool fp_plain_lt_p(const fp_t& a) {
   uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < NL; i++) {
-    uint64_t d = (uint64_t)a.l[i] - P_MOD.l[i] - borrow;
-    borrow = (uint32_t)(d >> 63);
-  }
+  for (int i = 0; i < NL; i++) (void)subb32(a.l[i], P_MOD.l[i], borrow, borrow);
   return borrow != 0;
 }
 
@@ -583,10 +580,7 @@ BGV_HD bool fp_plain_lt_p(const fp_t& a) {
 BGV_HD bool fp_plain_gt_half(const fp_t& a) {
   uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < NL; i++) {
-    uint64_t d = (uint64_t)P_HALF.l[i] - a.l[i] - borrow;
-    borrow = (uint32_t)(d >> 63);
-  }
+  for (int i = 0; i < NL; i++) (void)subb32(P_HALF.l[i], a.l[i], borrow, borrow);
   return borrow != 0;  // (p-1)/2 - a < 0
 }
 

@@ -62,11 +62,7 @@ BGV_HD void fp_half_shift(fp_t& r, const fp_t& a) {
   uint32_t t[NL];
   uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < NL; i++) {
-    const uint64_t s = (uint64_t)a.l[i] + (P_MOD.l[i] & m) + c;
-    t[i] = (uint32_t)s;
-    c = (uint32_t)(s >> 32);
-  }
+  for (int i = 0; i < NL; i++) t[i] = addc32(a.l[i], P_MOD.l[i] & m, c, c);
 #pragma unroll
   for (int i = 0; i < NL - 1; i++) r.l[i] = (t[i] >> 1) | (t[i + 1] << 31);
   r.l[NL - 1] = t[NL - 1] >> 1;
