@@ -39,6 +39,9 @@
 #ifndef BGV_FP6_INLINE
 #define BGV_FP6_INLINE 1
 #endif
+#ifndef BGV_POINT_INLINE
+#define BGV_POINT_INLINE 1  // jac_dbl / jac_add / jac_add_aff: 2049k -> 2155k sets/s
+#endif
 #ifndef BGV_MILLER_WAVES
 #define BGV_MILLER_WAVES 1
 #endif

@@ -10,6 +10,15 @@
 #pragma once
 #include "fp12.h"
 
+// point additions/doublings: inlined into the bulk kernels (BGV_POINT_INLINE,
+// bgv_kernels.hip) so their Fp2 temporaries stay in registers around the
+// register-ABI product leaf; non-inlined elsewhere
+#if defined(__HIPCC__) && BGV_POINT_INLINE
+#define BGV_NIP BGV_HD
+#else
+#define BGV_NIP BGV_NI
+#endif
+
 namespace bgv {
 
 // ---- field overloads used by the generic point code ------------------------
@@ -57,7 +66,7 @@ template <class F> BGV_HD void jac_neg(jac_t<F>& r, const jac_t<F>& p) {
 }
 
 // dbl-2009-l (a = 0): 2M + 5S
-template <class F> BGV_NI void jac_dbl(jac_t<F>& r, const jac_t<F>& p) {
+template <class F> BGV_NIP void jac_dbl(jac_t<F>& r, const jac_t<F>& p) {
   F A, B, C, D, E, Fq, t;
   fe_sqr(A, p.x);
   fe_sqr(B, p.y);
@@ -83,7 +92,7 @@ template <class F> BGV_NI void jac_dbl(jac_t<F>& r, const jac_t<F>& p) {
 }
 
 // add-2007-bl with the exceptional cases (infinity, P == Q, P == -Q)
-template <class F> BGV_NI void jac_add(jac_t<F>& r, const jac_t<F>& p, const jac_t<F>& q) {
+template <class F> BGV_NIP void jac_add(jac_t<F>& r, const jac_t<F>& p, const jac_t<F>& q) {
   if (jac_is_inf(p)) { r = q; return; }
   if (jac_is_inf(q)) { r = p; return; }
   F z1z1, z2z2, u1, u2, s1, s2, h, i, j, rr, v, t;
@@ -126,7 +135,7 @@ template <class F> BGV_NI void jac_add(jac_t<F>& r, const jac_t<F>& p, const jac
 }
 
 // madd-2007-bl: Jacobian + affine (q not infinity), with exceptional cases
-template <class F> BGV_NI void jac_add_aff(jac_t<F>& r, const jac_t<F>& p, const aff_t<F>& q) {
+template <class F> BGV_NIP void jac_add_aff(jac_t<F>& r, const jac_t<F>& p, const aff_t<F>& q) {
   if (jac_is_inf(p)) { jac_from_aff(r, q); return; }
   F z1z1, u2, s2, h, hh, i, j, rr, v, t;
   fe_sqr(z1z1, p.z);

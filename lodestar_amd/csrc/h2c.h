@@ -10,6 +10,12 @@
 #pragma once
 #include "curve.h"
 
+#if defined(__HIPCC__) && BGV_H2C_INLINE
+#define BGV_NIH BGV_HD
+#else
+#define BGV_NIH BGV_NI
+#endif
+
 namespace bgv {
 
 BGV_CONST uint32_t SHA256_K[64] = {
@@ -146,7 +152,7 @@ BGV_HD void hash_to_field_fp2x2(fp2_t& u0, fp2_t& u1, const uint8_t msg[32]) {
 }
 
 // simplified SWU onto E2' (RFC 9380 6.6.2), affine output
-BGV_NI void map_to_curve_sswu(g2a& out, const fp2_t& u) {
+BGV_NIH void map_to_curve_sswu(g2a& out, const fp2_t& u) {
   fp2_t u2, zu2, den, tv1, x1, x2, gx1, gx2, t;
   fp2_sqr(u2, u);
   fp2_mul(zu2, SSWU_Z, u2);
@@ -210,7 +216,7 @@ BGV_HD void fp2_horner(fp2_t& r, const fp2_t (&c)[N], const fp2_t& x) {
 
 // 3-isogeny E2' -> E2 straight into Jacobian coordinates (no inversion):
 // Z = xden yden, X = xnum xden yden^2, Y = y ynum xden^3 yden^2
-BGV_NI void iso_map_g2(g2j& r, const g2a& p) {
+BGV_NIH void iso_map_g2(g2j& r, const g2a& p) {
   fp2_t xn, xd, yn, yd, t, yd2;
   fp2_horner(xn, ISO_XNUM, p.x);
   fp2_horner(xd, ISO_XDEN, p.x);
