@@ -1,0 +1,367 @@
+/* N-API addon over libbgv.so: the binding a Lodestar maintainer adds beside
+ * chain/bls/multithread.  Plain C against
+ * node_api.h (N-API v4+, Node >= 12), no node-addon-api / C++ wrapper.
+ *
+ *   abiVersion() -> number                      bgv_abi_version
+ *   codeName(code) -> "BLST_..."                 bgv_set_code_name
+ *   open(device) -> ctx (external)               bgv_open      (multithread/index.ts:120)
+ *   close(ctx)                                   bgv_close     (multithread/index.ts:193-214)
+ *   pubkeysSet(ctx, first, Uint8Array, format)   bgv_pubkeys_set (pubkeyCache.ts:56-77)
+ *   pubkeysCount(ctx) -> number
+ *   pubkeysValidate(ctx, Uint8Array) -> Int32Array   bgv_pubkeys_validate (processDeposit.ts:57-66)
+ *   verify(ctx, batch) -> Promise<Int32Array>    bgv_verify on the libuv pool (worker.ts:30-106)
+ *   verifySync(ctx, batch) -> Int32Array         verifyOnMainThread / BlsSingleThreadVerifier
+ *
+ * batch = {jobOffsets: Uint32Array, pkOffsets: Uint32Array, pkIndices:
+ * Uint32Array, msgs: Uint8Array, sigs: Uint8Array (192 B per set), sigLen:
+ * Uint32Array, rawPks?: Uint8Array (96 B per key)}.  Per-job results are
+ * bgv_job_result values: 1 valid, 0 invalid, -code rejected.  Inputs are
+ * pinned by references until the async work completes; the library copies
+ * them to HBM and keeps nothing (SURVEY section 8b ownership).  A context is
+ * not thread-safe, so calls on one context are serialised by its mutex. */
+#include <node_api.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "bgv.h"
+
+#define NAPI_CALL(env, call)                                              \
+  do {                                                                    \
+    if ((call) != napi_ok) {                                              \
+      napi_throw_error((env), NULL, "bgv addon: N-API call failed: " #call); \
+      return NULL;                                                        \
+    }                                                                     \
+  } while (0)
+
+typedef struct {
+  bgv_ctx* ctx;
+  pthread_mutex_t mu;
+  int closed;
+} addon_ctx;
+
+static void ctx_finalize(napi_env env, void* data, void* hint) {
+  (void)env;
+  (void)hint;
+  addon_ctx* c = (addon_ctx*)data;
+  if (!c->closed) bgv_close(c->ctx);
+  pthread_mutex_destroy(&c->mu);
+  free(c);
+}
+
+static napi_value throw_bgv(napi_env env, int status) {
+  char msg[512];
+  snprintf(msg, sizeof msg, "bgv error %d: %s", status, bgv_last_error());
+  napi_throw_error(env, NULL, msg);
+  return NULL;
+}
+
+static addon_ctx* get_ctx(napi_env env, napi_value v) {
+  void* p = NULL;
+  if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
+    napi_throw_type_error(env, NULL, "expected a bgv context");
+    return NULL;
+  }
+  addon_ctx* c = (addon_ctx*)p;
+  if (c->closed) {
+    napi_throw_error(env, "QUEUE_ABORTED", "bgv context closed");
+    return NULL;
+  }
+  return c;
+}
+
+/* typed-array view: data pointer and element count; -1 on type error */
+static int typed(napi_env env, napi_value v, napi_typedarray_type want, void** data, size_t* len) {
+  bool is = false;
+  if (napi_is_typedarray(env, v, &is) != napi_ok || !is) return -1;
+  napi_typedarray_type t;
+  napi_value ab;
+  size_t off;
+  if (napi_get_typedarray_info(env, v, &t, len, data, &ab, &off) != napi_ok || t != want) return -1;
+  return 0;
+}
+
+/* ------------------------------------------------------------------ sync */
+static napi_value AbiVersion(napi_env env, napi_callback_info info) {
+  (void)info;
+  napi_value r;
+  NAPI_CALL(env, napi_create_int32(env, bgv_abi_version(), &r));
+  return r;
+}
+
+static napi_value CodeName(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value a[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, a, NULL, NULL));
+  int32_t code = 0;
+  NAPI_CALL(env, napi_get_value_int32(env, a[0], &code));
+  napi_value r;
+  NAPI_CALL(env, napi_create_string_utf8(env, bgv_set_code_name(code), NAPI_AUTO_LENGTH, &r));
+  return r;
+}
+
+static napi_value Open(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value a[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, a, NULL, NULL));
+  int32_t dev = 0;
+  if (argc >= 1) NAPI_CALL(env, napi_get_value_int32(env, a[0], &dev));
+  bgv_ctx* ctx = NULL;
+  const int st = bgv_open(dev, &ctx);
+  if (st != BGV_OK) return throw_bgv(env, st);
+  addon_ctx* c = (addon_ctx*)calloc(1, sizeof *c);
+  c->ctx = ctx;
+  pthread_mutex_init(&c->mu, NULL);
+  napi_value r;
+  NAPI_CALL(env, napi_create_external(env, c, ctx_finalize, NULL, &r));
+  return r;
+}
+
+static napi_value Close(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value a[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, a, NULL, NULL));
+  addon_ctx* c = get_ctx(env, a[0]);
+  if (!c) return NULL;
+  pthread_mutex_lock(&c->mu);  /* waits for in-flight work */
+  c->closed = 1;
+  bgv_close(c->ctx);
+  pthread_mutex_unlock(&c->mu);
+  return NULL;
+}
+
+static napi_value PubkeysSet(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value a[4];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, a, NULL, NULL));
+  addon_ctx* c = get_ctx(env, a[0]);
+  if (!c) return NULL;
+  uint32_t first = 0, fmt = 0;
+  NAPI_CALL(env, napi_get_value_uint32(env, a[1], &first));
+  NAPI_CALL(env, napi_get_value_uint32(env, a[3], &fmt));
+  void* data;
+  size_t len;
+  if (typed(env, a[2], napi_uint8_array, &data, &len)) {
+    napi_throw_type_error(env, NULL, "pubkeys must be a Uint8Array");
+    return NULL;
+  }
+  const size_t w = fmt == BGV_PK_UNCOMPRESSED_96 ? 96 : 48;
+  pthread_mutex_lock(&c->mu);
+  const int st = bgv_pubkeys_set(c->ctx, first, (uint32_t)(len / w), (const uint8_t*)data, fmt);
+  pthread_mutex_unlock(&c->mu);
+  if (st != BGV_OK) return throw_bgv(env, st);
+  return NULL;
+}
+
+static napi_value PubkeysCount(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value a[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, a, NULL, NULL));
+  addon_ctx* c = get_ctx(env, a[0]);
+  if (!c) return NULL;
+  uint32_t n = 0;
+  pthread_mutex_lock(&c->mu);
+  const int st = bgv_pubkeys_count(c->ctx, &n);
+  pthread_mutex_unlock(&c->mu);
+  if (st != BGV_OK) return throw_bgv(env, st);
+  napi_value r;
+  NAPI_CALL(env, napi_create_uint32(env, n, &r));
+  return r;
+}
+
+static napi_value new_int32_array(napi_env env, const int32_t* src, size_t n) {
+  void* dst = NULL;
+  napi_value ab, arr;
+  NAPI_CALL(env, napi_create_arraybuffer(env, 4 * n, &dst, &ab));
+  if (n) memcpy(dst, src, 4 * n);
+  NAPI_CALL(env, napi_create_typedarray(env, napi_int32_array, n, ab, 0, &arr));
+  return arr;
+}
+
+static napi_value PubkeysValidate(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value a[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, a, NULL, NULL));
+  addon_ctx* c = get_ctx(env, a[0]);
+  if (!c) return NULL;
+  void* data;
+  size_t len;
+  if (typed(env, a[1], napi_uint8_array, &data, &len)) {
+    napi_throw_type_error(env, NULL, "pubkeys must be a Uint8Array of 48-byte keys");
+    return NULL;
+  }
+  const uint32_t n = (uint32_t)(len / 48);
+  int32_t* codes = (int32_t*)calloc(n ? n : 1, 4);
+  pthread_mutex_lock(&c->mu);
+  const int st = bgv_pubkeys_validate(c->ctx, (const uint8_t*)data, n, codes);
+  pthread_mutex_unlock(&c->mu);
+  if (st != BGV_OK) {
+    free(codes);
+    return throw_bgv(env, st);
+  }
+  napi_value r = new_int32_array(env, codes, n);
+  free(codes);
+  return r;
+}
+
+/* ----------------------------------------------------------------- verify */
+enum { F_JOB, F_PKO, F_PKI, F_MSG, F_SIG, F_LEN, F_RAW, N_FIELDS };
+static const char* FIELD[N_FIELDS] = {"jobOffsets", "pkOffsets", "pkIndices", "msgs", "sigs", "sigLen", "rawPks"};
+static const napi_typedarray_type FIELD_T[N_FIELDS] = {napi_uint32_array, napi_uint32_array, napi_uint32_array,
+                                                       napi_uint8_array,  napi_uint8_array,  napi_uint32_array,
+                                                       napi_uint8_array};
+
+typedef struct {
+  addon_ctx* c;
+  bgv_batch b;
+  int32_t* job_result;
+  int status;
+  char err[512];
+  napi_ref refs[N_FIELDS];
+  napi_async_work work;
+  napi_deferred deferred;
+} verify_job;
+
+/* reads the batch object into j->b; pins the arrays when pin != 0 */
+static int read_batch(napi_env env, napi_value obj, verify_job* j, int pin) {
+  void* p[N_FIELDS] = {0};
+  size_t n[N_FIELDS] = {0};
+  for (int k = 0; k < N_FIELDS; k++) {
+    napi_value v;
+    bool has = false;
+    napi_has_named_property(env, obj, FIELD[k], &has);
+    if (!has) {
+      if (k == F_RAW) continue;
+      napi_throw_type_error(env, NULL, "batch field missing");
+      return -1;
+    }
+    napi_get_named_property(env, obj, FIELD[k], &v);
+    if (typed(env, v, FIELD_T[k], &p[k], &n[k])) {
+      napi_throw_type_error(env, NULL, "batch field has the wrong typed-array type");
+      return -1;
+    }
+    if (pin) napi_create_reference(env, v, 1, &j->refs[k]);
+  }
+  if (n[F_JOB] < 1 || n[F_PKO] < 1) {
+    napi_throw_range_error(env, NULL, "jobOffsets / pkOffsets need at least one entry");
+    return -1;
+  }
+  memset(&j->b, 0, sizeof j->b);
+  j->b.n_jobs = (uint32_t)(n[F_JOB] - 1);
+  j->b.n_sets = (uint32_t)(n[F_PKO] - 1);
+  if (n[F_MSG] < 32ull * j->b.n_sets || n[F_SIG] < 192ull * j->b.n_sets || n[F_LEN] < j->b.n_sets) {
+    napi_throw_range_error(env, NULL, "msgs / sigs / sigLen shorter than the set count");
+    return -1;
+  }
+  j->b.job_offsets = (const uint32_t*)p[F_JOB];
+  j->b.pk_offsets = (const uint32_t*)p[F_PKO];
+  j->b.pk_indices = (const uint32_t*)p[F_PKI];
+  j->b.msgs = (const uint8_t*)p[F_MSG];
+  j->b.sigs = (const uint8_t*)p[F_SIG];
+  j->b.sig_len = (const uint32_t*)p[F_LEN];
+  j->b.raw_pks = (const uint8_t*)p[F_RAW];
+  j->b.n_raw = (uint32_t)(n[F_RAW] / 96);
+  j->b.scalars = NULL; /* getrandom() inside the library */
+  j->b.on_device = 0;
+  return 0;
+}
+
+static void run_verify(verify_job* j) {
+  pthread_mutex_lock(&j->c->mu);
+  if (j->c->closed) {
+    j->status = BGV_E_INVALID_ARG;
+    snprintf(j->err, sizeof j->err, "QUEUE_ABORTED");
+  } else {
+    j->status = bgv_verify(j->c->ctx, &j->b, j->job_result, NULL, NULL);
+    if (j->status != BGV_OK) snprintf(j->err, sizeof j->err, "bgv error %d: %s", j->status, bgv_last_error());
+  }
+  pthread_mutex_unlock(&j->c->mu);
+}
+
+static void exec_verify(napi_env env, void* data) { /* libuv worker thread */
+  (void)env;
+  run_verify((verify_job*)data);
+}
+
+static void done_verify(napi_env env, napi_status st, void* data) { /* main thread */
+  verify_job* j = (verify_job*)data;
+  if (st != napi_ok && j->status == BGV_OK) {
+    j->status = BGV_E_INVALID_ARG;
+    snprintf(j->err, sizeof j->err, "async work cancelled");
+  }
+  if (j->status != BGV_OK) {
+    napi_value msg, err;
+    napi_create_string_utf8(env, j->err, NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, NULL, msg, &err);
+    napi_reject_deferred(env, j->deferred, err);
+  } else {
+    napi_value arr = new_int32_array(env, j->job_result, j->b.n_jobs);
+    napi_resolve_deferred(env, j->deferred, arr);
+  }
+  for (int k = 0; k < N_FIELDS; k++)
+    if (j->refs[k]) napi_delete_reference(env, j->refs[k]); /* unpin the inputs */
+  napi_delete_async_work(env, j->work);
+  free(j->job_result);
+  free(j);
+}
+
+static napi_value Verify(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value a[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, a, NULL, NULL));
+  addon_ctx* c = get_ctx(env, a[0]);
+  if (!c) return NULL;
+  verify_job* j = (verify_job*)calloc(1, sizeof *j);
+  j->c = c;
+  if (read_batch(env, a[1], j, 1)) {
+    for (int k = 0; k < N_FIELDS; k++)
+      if (j->refs[k]) napi_delete_reference(env, j->refs[k]);
+    free(j);
+    return NULL;
+  }
+  j->job_result = (int32_t*)calloc(j->b.n_jobs ? j->b.n_jobs : 1, 4);
+  napi_value promise, name;
+  NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
+  NAPI_CALL(env, napi_create_string_utf8(env, "bgv_verify", NAPI_AUTO_LENGTH, &name));
+  NAPI_CALL(env, napi_create_async_work(env, NULL, name, exec_verify, done_verify, j, &j->work));
+  NAPI_CALL(env, napi_queue_async_work(env, j->work));
+  return promise;
+}
+
+static napi_value VerifySync(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value a[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, a, NULL, NULL));
+  addon_ctx* c = get_ctx(env, a[0]);
+  if (!c) return NULL;
+  verify_job j;
+  memset(&j, 0, sizeof j);
+  j.c = c;
+  if (read_batch(env, a[1], &j, 0)) return NULL;
+  j.job_result = (int32_t*)calloc(j.b.n_jobs ? j.b.n_jobs : 1, 4);
+  run_verify(&j);
+  napi_value r = NULL;
+  if (j.status != BGV_OK) napi_throw_error(env, NULL, j.err);
+  else r = new_int32_array(env, j.job_result, j.b.n_jobs);
+  free(j.job_result);
+  return r;
+}
+
+static napi_value Init(napi_env env, napi_value exports) {
+  napi_property_descriptor d[] = {
+      {"abiVersion", NULL, AbiVersion, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"codeName", NULL, CodeName, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"open", NULL, Open, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"close", NULL, Close, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"pubkeysSet", NULL, PubkeysSet, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"pubkeysCount", NULL, PubkeysCount, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"pubkeysValidate", NULL, PubkeysValidate, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"verify", NULL, Verify, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"verifySync", NULL, VerifySync, NULL, NULL, NULL, napi_enumerable, NULL},
+  };
+  if (napi_define_properties(env, exports, sizeof d / sizeof d[0], d) != napi_ok) return NULL;
+  return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, Init)

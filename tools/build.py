@@ -51,6 +51,28 @@ def build(force=False, verbose=False, lib=LIB, defines=()):
     return lib
 
 
+NAPI_DIR = os.path.join(ROOT, "lodestar_amd", "napi")
+ADDON = os.path.join(NAPI_DIR, "bgv.node")
+NODE_INCLUDE = [d for d in ("/usr/include/node", "/usr/include/nodejs/src") if os.path.exists(os.path.join(d, "node_api.h"))]
+
+
+def build_addon(force=False):
+    """N-API addon lodestar_amd/napi/bgv.node over libbgv.so (INTEGRATION.md
+    section 3).  gcc against the system node_api.h; rpath points at the
+    library one directory up.  Returns None when no Node headers exist."""
+    if not NODE_INCLUDE:
+        return None
+    src = os.path.join(NAPI_DIR, "bgv_addon.c")
+    if (not force and os.path.exists(ADDON) and os.path.getmtime(ADDON) >= os.path.getmtime(src)
+            and os.path.getmtime(ADDON) >= os.path.getmtime(os.path.join(ROOT, "include", "bgv.h"))):
+        return ADDON
+    build()
+    subprocess.check_call(["gcc", "-O2", "-shared", "-fPIC", "-Wall", "-DNODE_GYP_MODULE_NAME=bgv",
+                           "-I" + NODE_INCLUDE[0], "-I" + os.path.join(ROOT, "include"), src, "-o", ADDON,
+                           "-L" + os.path.dirname(LIB), "-lbgv", "-lpthread", "-Wl,-rpath,$ORIGIN/.."])
+    return ADDON
+
+
 if __name__ == "__main__":
     if "--variant" in sys.argv:  # --variant NAME DEF [DEF ...]
         k = sys.argv.index("--variant")
@@ -62,3 +84,4 @@ if __name__ == "__main__":
     else:
         build(force="--force" in sys.argv, verbose=True)
         print(LIB)
+        print(build_addon(force="--force" in sys.argv))
