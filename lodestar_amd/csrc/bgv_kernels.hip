@@ -230,7 +230,10 @@ __global__ void BGV_BULK k_chunk_set(dev_batch b, dev_work w) {
   for (uint32_t c = w.chunk_off[i]; c < w.chunk_off[i + 1]; c++) w.chunk_set[c] = i;
 }
 
-__global__ void __launch_bounds__(64, BGV_PK_WAVES) k_pk_chunk(dev_batch b, dev_work w) {
+#ifndef BGV_PKC_WAVES
+#define BGV_PKC_WAVES BGV_PK_WAVES
+#endif
+__global__ void __launch_bounds__(64, BGV_PKC_WAVES) k_pk_chunk(dev_batch b, dev_work w) {
   const uint32_t g = gtid();
   if (g >= w.chunk_off[b.n_sets]) return;
   const uint32_t i = w.chunk_set[g];
