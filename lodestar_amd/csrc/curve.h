@@ -18,6 +18,13 @@
 #else
 #define BGV_NIP BGV_NI
 #endif
+// scalar-multiplication-level routines (x-chains, subgroup / cofactor maps,
+// affine conversion): BGV_CURVE_INLINE inlines them too (A/B knob)
+#if defined(__HIPCC__) && BGV_CURVE_INLINE
+#define BGV_NIC BGV_HD
+#else
+#define BGV_NIC BGV_NI
+#endif
 
 namespace bgv {
 
@@ -213,7 +220,7 @@ template <class F> BGV_NI void jac_mul_u64_w4(jac_t<F>& r, const jac_t<F>& p, ui
 }
 
 // [|x|]P for the BLS parameter (Hamming weight 6)
-template <class F> BGV_NI void jac_mul_abs_x(jac_t<F>& r, const jac_t<F>& p) {
+template <class F> BGV_NIC void jac_mul_abs_x(jac_t<F>& r, const jac_t<F>& p) {
   jac_t<F> acc = p;
   for (int b = 62; b >= 0; b--) {
     jac_dbl(acc, acc);
@@ -222,7 +229,7 @@ template <class F> BGV_NI void jac_mul_abs_x(jac_t<F>& r, const jac_t<F>& p) {
   r = acc;
 }
 
-template <class F> BGV_NI bool jac_to_aff(aff_t<F>& r, const jac_t<F>& p) {
+template <class F> BGV_NIC bool jac_to_aff(aff_t<F>& r, const jac_t<F>& p) {
   if (jac_is_inf(p)) { fe_zero(r.x); fe_zero(r.y); return false; }
   F zi, zi2, zi3;
   fe_inv(zi, p.z);
@@ -234,7 +241,7 @@ template <class F> BGV_NI bool jac_to_aff(aff_t<F>& r, const jac_t<F>& p) {
 }
 
 // equality of two Jacobian points (cross-multiplied)
-template <class F> BGV_NI bool jac_eq(const jac_t<F>& p, const jac_t<F>& q) {
+template <class F> BGV_NIC bool jac_eq(const jac_t<F>& p, const jac_t<F>& q) {
   const bool pi = jac_is_inf(p), qi = jac_is_inf(q);
   if (pi || qi) return pi && qi;
   F z1z1, z2z2, a, b;
@@ -275,7 +282,7 @@ BGV_HD void g2_psi2(g2j& r, const g2j& p) {
 }
 
 // Scott's test: P in G2  <=>  psi(P) == [x]P  (x = -|x|)
-BGV_NI bool g2_in_subgroup(const g2j& p) {
+BGV_NIC bool g2_in_subgroup(const g2j& p) {
   if (jac_is_inf(p)) return true;
   g2j xp, ps;
   jac_mul_abs_x(xp, p);
@@ -294,7 +301,7 @@ BGV_HD bool g2_aff_on_curve(const g2a& a) {
 }
 
 // h_eff [P] = [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P)  (Budroni-Pintore)
-BGV_NI void g2_clear_cofactor(g2j& r, const g2j& p) {
+BGV_NIC void g2_clear_cofactor(g2j& r, const g2j& p) {
   g2j t1, t2, t3, np;
   jac_mul_abs_x(t1, p);
   jac_neg(t1, t1);            // [x]P
