@@ -65,6 +65,8 @@ struct bgv_ctx {
   int miller_mode = -1;  // BGV_MILLER=serial|coop forces one Miller kernel (A/B tests); -1 = by batch size
   int msm_mode = -1;     // BGV_MSM=0|1 forces the signature combination (A/B tests); -1 = by batch shape
   bool overlap = true;    // BGV_OVERLAP=0 runs every stage on one stream (A/B tests)
+  int pairs = 0;          // BGV_PAIRS=1|2 forces sets per Miller work item (A/B tests); 0 = by batch size
+  int sched = 0;          // BGV_SCHED bit mask of extra stream waits (A/B tests, run_stages)
   hipStream_t st = nullptr, st_hash = nullptr, st_pk = nullptr;
   hipEvent_t ev[ST_COUNT + 1] = {};   // ev[s] = start of stage s on its stream
   hipEvent_t ev_end[ST_COUNT] = {};   // end of stage s on its stream
@@ -138,6 +140,8 @@ int bgv_open(int device, bgv_ctx** out) {
   if (const char* m = getenv("BGV_MILLER")) c->miller_mode = strcmp(m, "serial") != 0 ? 1 : 0;
   if (const char* m = getenv("BGV_MSM")) c->msm_mode = strcmp(m, "0") != 0 ? 1 : 0;
   if (const char* o = getenv("BGV_OVERLAP")) c->overlap = strcmp(o, "0") != 0;
+  if (const char* o = getenv("BGV_SCHED")) c->sched = atoi(o);
+  if (const char* o = getenv("BGV_PAIRS")) c->pairs = atoi(o);
   // hash -> set-pair Miller is the critical path: its stream (and the pubkey
   // stream feeding it) get the highest priority, signature decode/scaling the
   // lowest (it only feeds the signature tree and the 1 pair per job)
@@ -343,6 +347,7 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, std::vector<uin
   // (>= 65536 sets ~ 2 waves per SIMD at 1 pair per lane); below that the
   // per-lane latency of a longer item dominates
   d.pairs_per_item = n >= 65536 ? 2 : 1;
+  if (c->pairs == 1 || c->pairs == 2) d.pairs_per_item = (uint32_t)c->pairs;
   // six-lane cooperative Miller loop (low latency) unless the batch alone
   // fills the GPU, where the one-lane loop does less work per pair
   d.miller_coop = c->miller_mode >= 0 ? (uint32_t)c->miller_mode : (n < 65536 ? 1u : 0u);
@@ -412,13 +417,23 @@ static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int fro
     HIPCHK(hipStreamWaitEvent(c->st_hash, c->ev_fork, 0));
     HIPCHK(hipStreamWaitEvent(c->st_pk, c->ev_fork, 0));
   }
-  for (int s = from; s < to; s++) {
+  int order[ST_COUNT], n_order = 0;
+  for (int s = from; s < to; s++) order[n_order++] = s;
+  if (fork && (c->sched & 2) && from == ST_SIG) {  // enqueue sig after hash/pk so it can wait on them
+    order[0] = ST_HASH; order[1] = ST_PK; order[2] = ST_SIG;
+  }
+  for (int oi = 0; oi < n_order; oi++) {
+    const int s = order[oi];
     hipStream_t st = c->st;
     if (fork) {
       if (s == ST_HASH || s == ST_MILLER) st = c->st_hash;
       if (s == ST_PK) st = c->st_pk;
       if (s == ST_S_TREE || s == ST_MILLER) HIPCHK(hipStreamWaitEvent(st, c->ev_end[ST_PK], 0));
       if (s == ST_F_TREE) HIPCHK(hipStreamWaitEvent(st, c->ev_end[ST_MILLER], 0));
+      // A/B knobs: hold the signature leg back so hash/pk (the Miller inputs) get the chip first
+      if (s == ST_SIG_SCALE && (c->sched & 1)) HIPCHK(hipStreamWaitEvent(st, c->ev_end[ST_HASH], 0));
+      if (s == ST_SIG && (c->sched & 2)) HIPCHK(hipStreamWaitEvent(st, c->ev_end[ST_HASH], 0));
+      if (s == ST_SIG_SCALE && (c->sched & 4)) HIPCHK(hipStreamWaitEvent(st, c->ev_end[ST_PK], 0));
     }
     HIPCHK(hipEventRecord(c->ev[s], st));
     launch_stage(st, s, d, w);

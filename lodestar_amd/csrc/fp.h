@@ -290,7 +290,58 @@ BGV_HD void fp_mul28(fp_t& r, const fp_t& a, const fp_t& b) {
   fp_reduce_once(r, t);
 }
 
+// Squaring on the same digits: both operands are a << 4, so the square
+// carries the 2^8 of the pre-shift; the 91 cross products are summed once
+// against a doubled digit (2 A_j < 2^29), 105 digit products instead of 196.
+// Column bound: 7 cross terms < 2^57 + 1 square < 2^56 + 14 reduction terms
+// < 2^56 + carry < 2^61.  Inputs < 2^382 (lazy sums) as for fp_mul28; the
+// Montgomery sum stays < 1.5 p, so one subtraction leaves it canonical.
+BGV_HD void fp_sqr28(fp_t& r, const fp_t& a) {
+  uint32_t A[14], D[14];
+  unpack28<4>(A, a);
+#pragma unroll
+  for (int j = 0; j < 14; j++) D[j] = A[j] << 1;
+  uint64_t acc[28];
+#pragma unroll
+  for (int k = 0; k < 28; k++) acc[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    acc[2 * i] += (uint64_t)A[i] * A[i];
+#pragma unroll
+    for (int j = i + 1; j < 14; j++) acc[i + j] += (uint64_t)A[i] * D[j];
+  }
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    const uint32_t m = ((uint32_t)acc[i] * P28_INV) & M28;
+#pragma unroll
+    for (int j = 0; j < 14; j++) acc[i + j] += (uint64_t)m * P28[j];
+    acc[i + 1] += acc[i] >> 28;
+  }
+  uint32_t d[14];
+  uint64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 14; k++) {
+    const uint64_t v = acc[14 + k] + c;
+    d[k] = (uint32_t)v & M28;
+    c = v >> 28;
+  }
+  fp_t t;
+  pack28(t, d);
+  fp_reduce_once(r, t);
+}
+
 #if defined(__HIPCC__) && BGV_FPMUL_CALL
+static __device__ __noinline__ fp_vec_t fp_sqr_leaf(fp_vec_t a) {
+  fp_t x, r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) x.l[i] = a[i];
+  fp_sqr28(r, x);
+  fp_vec_t v;
+#pragma unroll
+  for (int i = 0; i < NL; i++) v[i] = r.l[i];
+  return v;
+}
+
 static __device__ __noinline__ fp_vec_t fp_mul_leaf(fp_vec_t a, fp_vec_t b) {
   fp_t x, y, r;
 #pragma unroll
@@ -306,7 +357,28 @@ static __device__ __noinline__ fp_vec_t fp_mul_leaf(fp_vec_t a, fp_vec_t b) {
 }
 #endif
 
-BGV_HD void fp_sqr(fp_t& r, const fp_t& a) { fp_mul(r, a, a); }
+#ifndef BGV_FPSQR
+#define BGV_FPSQR 1  // dedicated squaring (fp_sqr28); 0 = fp_mul(a, a)
+#endif
+BGV_HD void fp_sqr(fp_t& r, const fp_t& a) {
+#if BGV_FPSQR && BGV_FPMUL28
+#ifdef BGV_COUNT_OPS
+  bgv_fpmul_count++;
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && BGV_FPMUL_CALL
+  fp_vec_t va;
+#pragma unroll
+  for (int i = 0; i < NL; i++) va[i] = a.l[i];
+  const fp_vec_t vr = fp_sqr_leaf(va);
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.l[i] = vr[i];
+#else
+  fp_sqr28(r, a);
+#endif
+#else
+  fp_mul(r, a, a);
+#endif
+}
 
 // small multiples by repeated doubling/addition
 BGV_HD void fp_mul3(fp_t& r, const fp_t& a) { fp_t t; fp_add(t, a, a); fp_add(r, t, a); }

@@ -63,6 +63,13 @@ int hc_lazy_mul_canonical(uint64_t seed, int n) {
     fp_mul(r3, ap, b);
     for (int i = 0; i < NL; i++) if (r1.l[i] != r2.l[i] || r3.l[i] != r2.l[i]) { bad++; break; }
     if (!fp_plain_lt_p(r1)) bad++;
+    // dedicated squaring (fp_sqr28) against the product, canonical and lazy (< 2p) inputs
+    fp_t s1, s2, s3;
+    fp_mul28(s1, a, a);
+    fp_sqr28(s2, a);
+    fp_sqr28(s3, ap);
+    for (int i = 0; i < NL; i++) if (s1.l[i] != s2.l[i] || s1.l[i] != s3.l[i]) { bad++; break; }
+    if (!fp_plain_lt_p(s3)) bad++;
   }
   return bad;
 }
