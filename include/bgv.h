@@ -90,8 +90,9 @@ typedef struct bgv_ctx bgv_ctx;
  * reference's "BLST_INVALID_SIZE", e2e/chain/bls/multithread.test.ts:97).
  *
  * scalars: 64-bit non-zero random multipliers, one per set (blst
- * mul_n_aggregate randomness).  NULL = drawn from getrandom() inside the
- * library (production).  Tests inject them for reproducibility.
+ * mul_n_aggregate randomness).  NULL = drawn inside the library
+ * (production): ChaCha20 on the device, keyed per call by 32 bytes of
+ * getrandom().  Tests inject them for reproducibility.
  *
  * When `on_device` is non-zero every array pointer is a device pointer on
  * the context's device (inputs already resident in HBM); otherwise they are

@@ -254,15 +254,13 @@ int bgv_pubkeys_validate(bgv_ctx* c, const uint8_t* pk48, uint32_t n, int32_t* c
 
 // ---------------------------------------------------------------- batches
 
-static void random_scalars(uint64_t* s, uint32_t n) {
+static void random_bytes(void* out, size_t n) {
   size_t got = 0;
-  uint8_t* p = (uint8_t*)s;
-  while (got < (size_t)n * 8) {
-    ssize_t r = getrandom(p + got, (size_t)n * 8 - got, 0);
+  uint8_t* p = (uint8_t*)out;
+  while (got < n) {
+    ssize_t r = getrandom(p + got, n - got, 0);
     if (r > 0) got += (size_t)r;
   }
-  for (uint32_t i = 0; i < n; i++)
-    while (s[i] == 0) (void)getrandom(&s[i], 8, 0);  // blst needs non-zero randomness
 }
 
 template <class T>
@@ -361,9 +359,15 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, std::vector<uin
   } else if (b->scalars) {
     d.scalars = b->scalars;
   } else {
-    scal_host.resize(n ? n : 1);
-    random_scalars(scal_host.data(), n);
-    if (int r = stage_in(c, c->scalars, (const uint64_t*)scal_host.data(), (size_t)n, d.scalars)) return r;
+    // fresh 64-bit multipliers on the device: ChaCha20 keyed by 32 bytes of
+    // getrandom() (+ 12-byte nonce) per call, rng.h
+    (void)scal_host;
+    uint32_t kn[11];
+    random_bytes(kn, sizeof kn);
+    if (int r = c->scalars.ensure(n ? n : 1)) return r;
+    launch_gen_scalars(c->st, kn, kn + 8, c->scalars.p, n);
+    HIPCHK(hipGetLastError());
+    d.scalars = c->scalars.p;
   }
   return 0;
 }

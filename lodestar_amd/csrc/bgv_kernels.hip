@@ -537,6 +537,14 @@ __global__ void __launch_bounds__(64, BGV_WAVES) k_miller_coop(dev_batch b, dev_
   }
 }
 
+// per-set batch scalars (rng.h): one ChaCha20 block per set
+struct chacha_key { uint32_t key[8], nonce[3]; };
+__global__ void __launch_bounds__(64) k_gen_scalars(chacha_key k, uint64_t* out, uint32_t n) {
+  const uint32_t i = gtid();
+  if (i >= n) return;
+  out[i] = batch_scalar(k.key, i, k.nonce);
+}
+
 // set codes for the host: signature code first, then the pubkey code
 __global__ void BGV_BULK k_set_codes(dev_batch b, dev_work w) {
   const uint32_t i = gtid();
@@ -817,6 +825,12 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
 
 void launch_fp12_convert(hipStream_t st, const fp12_t* in, fp12_t* out, uint32_t n, bool to_mont) {
   BGV_LAUNCH(k_fp12_convert, n, in, out, n, to_mont ? 1u : 0u);
+}
+void launch_gen_scalars(hipStream_t st, const uint32_t key[8], const uint32_t nonce[3], uint64_t* out, uint32_t n) {
+  chacha_key k;
+  for (int i = 0; i < 8; i++) k.key[i] = key[i];
+  for (int i = 0; i < 3; i++) k.nonce[i] = nonce[i];
+  BGV_LAUNCH(k_gen_scalars, n, k, out, n);
 }
 void launch_gen_keys(hipStream_t st, g1a* table, uint32_t* sk, uint32_t first, uint32_t n, uint64_t seed) {
   BGV_LAUNCH(k_gen_keys, n, table, sk, first, n, seed);

@@ -6,6 +6,7 @@
 // coefficients ordered w^0.c0, w^0.c1, w^1.c0, ... (tower position k at w^k).
 #include <string.h>
 #include "../../lodestar_amd/csrc/pairing.h"
+#include "../../lodestar_amd/csrc/rng.h"
 
 using namespace bgv;
 
@@ -143,5 +144,12 @@ void hc_miller_add_step(const uint8_t* t288, const uint8_t* q192, const uint8_t*
   miller_add_step(T, a0, a1, b1, q, p.x, p.y);
   put_fp2(t_out288, T.x); put_fp2(t_out288 + 96, T.y); put_fp2(t_out288 + 192, T.z);
   put_fp2(line288, a0); put_fp2(line288 + 96, a1); put_fp2(line288 + 192, b1);
+}
+}
+
+extern "C" {
+// ChaCha20 block function of the device scalar generator (rng.h)
+void hc_chacha20_block(const uint32_t* key, uint32_t counter, const uint32_t* nonce, uint32_t* out) {
+  chacha20_block(out, key, counter, nonce);
 }
 }

@@ -267,3 +267,14 @@ def test_miller_loop2_equals_product_of_single_loops():
     lib.hc_fp12_mul(o1.raw, o2.raw, prod)
     lib.hc_miller_loop2(H.g1_b(P1), H.g2_b(Q1), H.g1_b(P2), H.g2_b(Q2), o12)
     assert o12.raw == prod.raw
+
+
+def test_chacha20_block_rfc8439():
+    """rng.h block function (the device batch-scalar generator) on the
+    RFC 8439 section 2.3.2 test vector."""
+    key = (ctypes.c_uint32 * 8)(*[int.from_bytes(bytes(range(4 * i, 4 * i + 4)), "little") for i in range(8)])
+    nonce = (ctypes.c_uint32 * 3)(0x09000000, 0x4A000000, 0x00000000)
+    out = (ctypes.c_uint32 * 16)()
+    lib.hc_chacha20_block(key, 1, nonce, out)
+    assert list(out) == [0xE4E7F110, 0x15593BD1, 0x1FDD0F50, 0xC47120A3, 0xC7F4D1C7, 0x0368C033, 0x9AAA2204, 0x4E6CD4C3,
+                         0x466482D2, 0x09AA9F07, 0x05D7C214, 0xA2028BD9, 0xD19C12B5, 0xB94E16DE, 0xE883D0CB, 0x4E3C50A2]
