@@ -385,7 +385,18 @@ BGV_HD void fp_mul3(fp_t& r, const fp_t& a) { fp_t t; fp_add(t, a, a); fp_add(r,
 BGV_HD void fp_mul4(fp_t& r, const fp_t& a) { fp_t t; fp_add(t, a, a); fp_add(r, t, t); }
 BGV_HD void fp_mul8(fp_t& r, const fp_t& a) { fp_t t; fp_add(t, a, a); fp_add(t, t, t); fp_add(r, t, t); }
 
-BGV_HD void fp_half(fp_t& r, const fp_t& a) { fp_mul(r, a, FP_HALF); }
+// a / 2 mod p by a shift: (a + (a odd ? p : 0)) >> 1  (a < p, so a + p < 2^382);
+// ~40 VALU instructions instead of a product by 1/2
+BGV_HD void fp_half(fp_t& r, const fp_t& a) {
+  const uint32_t m = 0u - (a.l[0] & 1u);
+  uint32_t t[NL];
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) t[i] = addc32(a.l[i], P_MOD.l[i] & m, c, c);
+#pragma unroll
+  for (int i = 0; i < NL - 1; i++) r.l[i] = (t[i] >> 1) | (t[i + 1] << 31);
+  r.l[NL - 1] = t[NL - 1] >> 1;
+}
 
 // r = a^e for a fixed public exponent e (12 x u32, plain integer).
 // Left-to-right binary over the exponent's bits; the bit test is uniform

@@ -56,17 +56,7 @@ BGV_CONST sq_term SQ_TAB[6][4] = {
     {{0, 5, 1, 0, 1}, {1, 4, 1, 0, 1}, {2, 3, 1, 0, 1}, {0, 0, 0, 0, 0}},
 };
 
-// a / 2 mod p by a shift: (a + (a odd ? p : 0)) >> 1  (a < p, so a + p < 2^382)
-BGV_HD void fp_half_shift(fp_t& r, const fp_t& a) {
-  const uint32_t m = 0u - (a.l[0] & 1u);
-  uint32_t t[NL];
-  uint32_t c = 0;
-#pragma unroll
-  for (int i = 0; i < NL; i++) t[i] = addc32(a.l[i], P_MOD.l[i] & m, c, c);
-#pragma unroll
-  for (int i = 0; i < NL - 1; i++) r.l[i] = (t[i] >> 1) | (t[i + 1] << 31);
-  r.l[NL - 1] = t[NL - 1] >> 1;
-}
+BGV_HD void fp_half_shift(fp_t& r, const fp_t& a) { fp_half(r, a); }
 
 __device__ __forceinline__ void fp2_half(fp2_t& r, const fp2_t& a) {
   fp_half_shift(r.c0, a.c0);

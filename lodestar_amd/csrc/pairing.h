@@ -18,6 +18,16 @@ namespace bgv {
 
 struct g2p_t { fp2_t x, y, z; };  // homogeneous projective: x = X/Z, y = Y/Z
 
+// r = 3b' a with b' = 4(1+i) (the twist E2: y^2 = x^3 + 4(1+i)): xi-multiply,
+// then x4 and x3 by additions instead of a product by the constant
+BGV_HD void fp2_mul_3b(fp2_t& r, const fp2_t& a) {
+  fp2_t t;
+  fp2_mul_xi(t, a);
+  fp2_dbl(t, t);
+  fp2_dbl(t, t);
+  fp2_mul3(r, t);
+}
+
 // T <- 2T, line tangent at T evaluated at P
 BGV_NIS void miller_dbl_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const fp_t& xp, const fp_t& yp) {
   fp2_t A, B, C, E, F, G, H, t;
@@ -26,7 +36,7 @@ BGV_NIS void miller_dbl_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const fp
   fp_half(A.c1, A.c1);           // A = XY/2
   fp2_sqr(B, T.y);               // Y^2
   fp2_sqr(C, T.z);               // Z^2
-  fp2_mul(E, C, B2_X3_MONT);     // 3b' Z^2
+  fp2_mul_3b(E, C);              // 3b' Z^2 (additions: 3b' = 12(1+i))
   fp2_mul3(F, E);                // 9b' Z^2
   fp2_add(t, T.y, T.z);
   fp2_sqr(t, t);
