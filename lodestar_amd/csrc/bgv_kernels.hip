@@ -448,45 +448,8 @@ __global__ void BGV_BULK k_item_job(dev_batch b, dev_work w) {
   for (uint32_t t = w.item_off[j]; t < w.item_off[j + 1]; t++) w.item_job[t] = j;
 }
 
-__global__ void __launch_bounds__(64, BGV_MILLER_WAVES) k_miller(dev_batch b, dev_work w, uint32_t jobs_part) {
-  const uint32_t n_items = w.item_off[b.n_jobs];
-  const uint32_t t = gtid() + (jobs_part ? n_items : 0u);
-  if (jobs_part ? t >= n_items + b.n_jobs : t >= n_items) return;
-  // the accumulator lives in LDS: at 1 wave/SIMD a lane has 640 B of it, and
-  // every fp12_sqr / fp12_mul_line call reads and writes f by reference, which
-  // from a stack slot would be ~3 KB of scratch traffic per lane per bit
-#if BGV_MILLER_LDS_F
-  __shared__ fp12_t f_lds[64];
-  fp12_t& f = f_lds[threadIdx.x];
-#else
-  fp12_t f;
-#endif
-  if (t < n_items) {
-    const uint32_t j = w.item_job[t];
-    const uint32_t i1 = b.job_off[j] + b.pairs_per_item * (t - w.item_off[j]);
-    const bool two = b.pairs_per_item == 2 && i1 + 1 < b.job_off[j + 1];
-    const bool ok1 = w.pk_code[i1] == C_OK;
-    const bool ok2 = !two || w.pk_code[i1 + 1] == C_OK;
-    // a parse error rejects the whole job, so its Miller values are never used;
-    // signature codes are not known yet (this part overlaps ST_SIG_SCALE)
-    if (!ok1 || !ok2) fp12_one(f);
-    else if (two) miller_loop2(f, w.rpk_aff[i1], w.h_aff[i1], w.rpk_aff[i1 + 1], w.h_aff[i1 + 1]);
-    else miller_loop(f, w.rpk_aff[i1], false, w.h_aff[i1], false);
-    w.f_set[i1] = f;
-    if (two) {
-      fp12_one(f);
-      w.f_set[i1 + 1] = f;
-    }
-  } else {
-    const uint32_t j = t - n_items;
-    g1a ng;
-    ng.x = G1_X_MONT;
-    ng.y = G1_NEG_Y_MONT;
-    if (w.job_code[j] != C_OK || w.s_inf[j]) fp12_one(f);
-    else miller_loop(f, ng, false, w.s_aff[j], false);
-    w.f_set[b.n_sets + j] = f;
-  }
-}
+// k_miller (the set-pair Miller loops) lives in bgv_miller.hip: that unit
+// uses the Fp2 product leaf with lazy reduction (fp2.h BGV_FP2_LEAF).
 
 // Cooperative variant (miller_coop.h): 10 pairs per 64-lane workgroup, six
 // lanes per pair, pair t < n_sets is (r_t PK_t, H(m_t)), then (-G1, S_job).
@@ -801,7 +764,7 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
           hipLaunchKernelGGL(k_miller_coop, dim3((b.n_sets + COOP_GROUPS - 1) / COOP_GROUPS), dim3(64), 0, st, b, w, 0u, b.n_sets);
         break;
       }
-      BGV_LAUNCH(k_miller, b.n_sets / b.pairs_per_item + b.n_jobs, b, w, 0u);  // >= items (launch_prep)
+      launch_miller(st, b, w);  // bgv_miller.hip
       break;
     case ST_MILLER_JOBS:  // (-G1, S_job) pairs: needs ST_S_TREE
       // always the six-lane loop: one pair per job is latency-bound (a lone

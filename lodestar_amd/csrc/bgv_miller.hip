@@ -1,0 +1,83 @@
+// The set-pair Miller loop kernel (k_miller), in its own translation unit so
+// that its Fp2 products can go through the Fp2 leaf with lazy reduction
+// (BGV_FP2_LEAF=1, fp.h fp2_mul28_lazy: 980 digit products per Fp2 product
+// instead of 3 x 392).  That leaf needs 248 VGPRs, which only this kernel
+// (1 wave/SIMD, 512-register budget) can give it.  Measured on MI355X:
+// k_miller 19.5 ms against 18.8-19.2 ms with the Fp leaf (the 16 operand
+// dwords past v31 travel through scratch and the signed 64-bit column
+// shifts cost hazard NOPs), so the knob is off.
+// Work items: every job's sets taken two at a time (one shared Fp12
+// accumulator and squaring per two pairs, miller_loop2), then one item per
+// job for its (-G1, S_job) pair.  Item offsets per job come from a scan
+// (bgv_kernels.hip k_item_count / k_item_job).
+#ifndef BGV_FP2_LEAF
+#define BGV_FP2_LEAF 0
+#endif
+#ifndef BGV_FPMUL_CALL
+#define BGV_FPMUL_CALL 1
+#endif
+#ifndef BGV_FP2_INLINE
+#define BGV_FP2_INLINE 1
+#endif
+#ifndef BGV_FP6_INLINE
+#define BGV_FP6_INLINE 1
+#endif
+#ifndef BGV_POINT_INLINE
+#define BGV_POINT_INLINE 1  // jac_dbl / jac_add / jac_add_aff: 2049k -> 2155k sets/s
+#endif
+#ifndef BGV_MILLER_WAVES
+#define BGV_MILLER_WAVES 1
+#endif
+#ifndef BGV_MILLER_LDS_F
+#define BGV_MILLER_LDS_F 1
+#endif
+#include "bgv_internal.h"
+
+namespace bgv {
+
+__global__ void __launch_bounds__(64, BGV_MILLER_WAVES) k_miller(dev_batch b, dev_work w, uint32_t jobs_part) {
+  const uint32_t n_items = w.item_off[b.n_jobs];
+  const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) + (jobs_part ? n_items : 0u);
+  if (jobs_part ? t >= n_items + b.n_jobs : t >= n_items) return;
+  // the accumulator lives in LDS: at 1 wave/SIMD a lane has 640 B of it, and
+  // every fp12_sqr / fp12_mul_line call reads and writes f by reference, which
+  // from a stack slot would be ~3 KB of scratch traffic per lane per bit
+#if BGV_MILLER_LDS_F
+  __shared__ fp12_t f_lds[64];
+  fp12_t& f = f_lds[threadIdx.x];
+#else
+  fp12_t f;
+#endif
+  if (t < n_items) {
+    const uint32_t j = w.item_job[t];
+    const uint32_t i1 = b.job_off[j] + b.pairs_per_item * (t - w.item_off[j]);
+    const bool two = b.pairs_per_item == 2 && i1 + 1 < b.job_off[j + 1];
+    const bool ok1 = w.pk_code[i1] == C_OK;
+    const bool ok2 = !two || w.pk_code[i1 + 1] == C_OK;
+    // a parse error rejects the whole job, so its Miller values are never used;
+    // signature codes are not known yet (this part overlaps ST_SIG_SCALE)
+    if (!ok1 || !ok2) fp12_one(f);
+    else if (two) miller_loop2(f, w.rpk_aff[i1], w.h_aff[i1], w.rpk_aff[i1 + 1], w.h_aff[i1 + 1]);
+    else miller_loop(f, w.rpk_aff[i1], false, w.h_aff[i1], false);
+    w.f_set[i1] = f;
+    if (two) {
+      fp12_one(f);
+      w.f_set[i1 + 1] = f;
+    }
+  } else {
+    const uint32_t j = t - n_items;
+    g1a ng;
+    ng.x = G1_X_MONT;
+    ng.y = G1_NEG_Y_MONT;
+    if (w.job_code[j] != C_OK || w.s_inf[j]) fp12_one(f);
+    else miller_loop(f, ng, false, w.s_aff[j], false);
+    w.f_set[b.n_sets + j] = f;
+  }
+}
+
+void launch_miller(hipStream_t st, const dev_batch& b, const dev_work& w) {
+  const uint32_t n = b.n_sets / b.pairs_per_item + b.n_jobs;  // >= items (launch_prep)
+  if (n) hipLaunchKernelGGL(k_miller, dim3((n + 63u) / 64u), dim3(64), 0, st, b, w, 0u);
+}
+
+}  // namespace bgv
