@@ -31,6 +31,13 @@
 #ifndef BGV_MILLER_LDS_F
 #define BGV_MILLER_LDS_F 1
 #endif
+// per-unit inlining knobs (A/B builds): Fp12 layer and Miller steps
+#ifdef BGV_MILLER_FP12_INLINE
+#define BGV_FP12_INLINE BGV_MILLER_FP12_INLINE
+#endif
+#ifdef BGV_MILLER_STEP_INLINE
+#define BGV_STEP_INLINE BGV_MILLER_STEP_INLINE
+#endif
 #include "bgv_internal.h"
 
 namespace bgv {
