@@ -65,6 +65,7 @@ struct bgv_ctx {
   int miller_mode = -1;  // BGV_MILLER=serial|coop forces one Miller kernel (A/B tests); -1 = by batch size
   int msm_mode = -1;     // BGV_MSM=0|1 forces the signature combination (A/B tests); -1 = by batch shape
   bool overlap = true;    // BGV_OVERLAP=0 runs every stage on one stream (A/B tests)
+  int split = -1;         // BGV_SPLIT=0|1 forces the latency mode (A/B tests); -1 = by batch size
   int pairs = 0;          // BGV_PAIRS=1|2 forces sets per Miller work item (A/B tests); 0 = by batch size
   int sched = 0;          // BGV_SCHED bit mask of extra stream waits (A/B tests, run_stages)
   hipStream_t st = nullptr, st_hash = nullptr, st_pk = nullptr;
@@ -87,7 +88,8 @@ struct bgv_ctx {
   dbuf<g1a> rpk_aff;
   dbuf<uint32_t> chunk_off, chunk_set;
   dbuf<g1j> pk_part;
-  dbuf<g2j> rsig;
+  dbuf<g2j> rsig, q_part;
+  dbuf<uint32_t> sig_grp;
   dbuf<fp12_t> f_set, f_job, f_batch, f_tmp, f_part;
   dbuf<uint32_t> set_job, s_inf, item_off, item_job;
   dbuf<g2a> s_aff;
@@ -142,6 +144,7 @@ int bgv_open(int device, bgv_ctx** out) {
   if (const char* o = getenv("BGV_OVERLAP")) c->overlap = strcmp(o, "0") != 0;
   if (const char* o = getenv("BGV_SCHED")) c->sched = atoi(o);
   if (const char* o = getenv("BGV_PAIRS")) c->pairs = atoi(o);
+  if (const char* o = getenv("BGV_SPLIT")) c->split = atoi(o) != 0 ? 1 : 0;
   // hash -> set-pair Miller is the critical path: its stream (and the pubkey
   // stream feeding it) get the highest priority, signature decode/scaling the
   // lowest (it only feeds the signature tree and the 1 pair per job)
@@ -174,7 +177,7 @@ int bgv_close(bgv_ctx* c) {
   c->scalars.release(); c->raw_conv.release();
   c->sig_aff.release(); c->h_aff.release(); c->sig_inf.release(); c->flags.release();
   c->sig_code.release(); c->pk_code.release(); c->job_code.release(); c->job_result.release(); c->set_code.release();
-  c->rpk_aff.release(); c->chunk_off.release(); c->chunk_set.release(); c->pk_part.release(); c->rsig.release(); c->f_set.release(); c->f_job.release(); c->f_batch.release(); c->f_tmp.release(); c->f_part.release();
+  c->rpk_aff.release(); c->chunk_off.release(); c->chunk_set.release(); c->pk_part.release(); c->rsig.release(); c->q_part.release(); c->sig_grp.release(); c->f_set.release(); c->f_job.release(); c->f_batch.release(); c->f_tmp.release(); c->f_part.release();
   c->msm_bucket.release(); c->msm_win.release(); c->msm_mask.release();
   c->set_job.release(); c->s_inf.release(); c->item_off.release(); c->item_job.release(); c->s_aff.release();
   c->mb_fp.release(); c->mb_u64.release();
@@ -346,6 +349,9 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, std::vector<uin
   // per-lane latency of a longer item dominates
   d.pairs_per_item = n >= 65536 ? 2 : 1;
   if (c->pairs == 1 || c->pairs == 2) d.pairs_per_item = (uint32_t)c->pairs;
+  // latency mode below one chip-full of lanes: hash maps on two lanes per
+  // set, subgroup check beside the signature scaling (bgv_kernels.hip)
+  d.split = c->split >= 0 ? (uint32_t)c->split : (n < 65536 ? 1u : 0u);
   // six-lane cooperative Miller loop (low latency) unless the batch alone
   // fills the GPU, where the one-lane loop does less work per pair
   d.miller_coop = c->miller_mode >= 0 ? (uint32_t)c->miller_mode : (n < 65536 ? 1u : 0u);
@@ -393,6 +399,11 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
   w.f_part = c->f_part.p; w.flags = c->flags.p;
   w.item_off = c->item_off.p; w.item_job = c->item_job.p;
   w.set_job = c->set_job.p; w.f_batch = c->f_batch.p; w.f_tmp = c->f_tmp.p; w.s_aff = c->s_aff.p; w.s_inf = c->s_inf.p;
+  w.q_part = nullptr; w.sig_grp = nullptr;
+  if (d.split) {
+    if ((r = c->q_part.ensure(2 * ns)) || (r = c->sig_grp.ensure(ns))) return r;
+    w.q_part = c->q_part.p; w.sig_grp = c->sig_grp.p;
+  }
   w.msm_bucket = nullptr; w.msm_mask = nullptr; w.msm_win = nullptr;
   if (d.msm) {
     if ((r = c->msm_bucket.ensure(nj * 16 * 15)) || (r = c->msm_mask.ensure(nj * 16)) || (r = c->msm_win.ensure(nj * 16))) return r;

@@ -21,6 +21,7 @@ struct dev_batch {
   uint32_t miller_coop;     // 1: six-lane cooperative Miller loop (miller_coop.h)
   uint32_t pairs_per_item;  // Miller pairs sharing one accumulator (1, or 2 for batches that fill the GPU)
   uint32_t msm;             // 1: per-job bucket MSM for sum r_i sigma_i (k_msm_*), 0: per-set [r_i] sigma_i + tree
+  uint32_t split;           // 1: latency mode: hash maps on two lanes per set, subgroup check beside [r_i] sigma_i
   const uint32_t* job_off;
   const uint32_t* pk_off;
   const uint32_t* pk_idx;
@@ -38,6 +39,8 @@ struct dev_work {
   uint32_t* sig_inf;  // signature is the identity
   int32_t* sig_code;  // parse / subgroup outcome
   g2a* h_aff;         // H(m)
+  g2j* q_part;        // [2 n_sets] split mode: the two mapped points of every message
+  uint32_t* sig_grp;  // split mode: signature passed the subgroup check
   g2j* msm_bucket;    // [n_jobs * 16 windows * 15 buckets] (msm mode)
   uint32_t* msm_mask; // [n_jobs * 16] occupied buckets of each (job, window)
   g2j* msm_win;       // [n_jobs * 16] window sums

@@ -160,6 +160,91 @@ __global__ void __launch_bounds__(64, BGV_SIG_WAVES) k_sig(dev_batch b, dev_work
   w.sig_code[i] = code;
 }
 
+// Latency mode (dev_batch.split, small batches): the decode runs alone, then
+// one launch runs the subgroup check and [r_i] sigma_i side by side (blocks
+// [0, nb) check, blocks [nb, 2 nb) scale: uniform per wave), so the
+// signature path's chain is decode + max(check, scale) instead of
+// decode + check + scale.  k_sig_fix folds the check into the codes.
+__global__ void __launch_bounds__(64, BGV_SIG_WAVES) k_sig_dec(dev_batch b, dev_work w) {
+  const uint32_t i = gtid();
+  if (i >= b.n_sets) return;
+  const uint32_t len = b.sig_len[i];
+  const uint8_t* s = b.sigs + 192u * i;
+  g2a a;
+  bool inf = false;
+  int32_t code;
+  if (len == 96u) code = g2_decompress(a, inf, s);
+  else if (len == 192u) code = g2_deserialize(a, inf, s);
+  else code = C_INVALID_SIZE;
+  if (code != C_OK || inf) { a.x = fp2_zero(); a.y = fp2_zero(); }
+  w.sig_aff[i] = a;
+  w.sig_inf[i] = inf ? 1u : 0u;
+  w.sig_code[i] = code;
+}
+
+__global__ void __launch_bounds__(64, BGV_SIG_WAVES) k_sig_split(dev_batch b, dev_work w) {
+  const uint32_t nb = (b.n_sets + 63u) / 64u;
+  const bool check = blockIdx.x < nb;
+  const uint32_t i = (check ? blockIdx.x : blockIdx.x - nb) * 64u + threadIdx.x;
+  if (i >= b.n_sets) return;
+  const bool live = w.sig_code[i] == C_OK && !w.sig_inf[i];  // decode outcome (k_sig_dec)
+  if (check) {
+    uint32_t ok = 1u;
+    if (live) {
+      g2j j;
+      jac_from_aff(j, w.sig_aff[i]);
+      ok = g2_in_subgroup(j) ? 1u : 0u;
+    }
+    w.sig_grp[i] = ok;
+  } else {
+    g2j r;
+    if (!live) {
+      jac_set_inf(r);
+    } else {
+      g2j s;
+      jac_from_aff(s, w.sig_aff[i]);
+      jac_mul_u64_w4(r, s, b.scalars[i]);
+    }
+    w.rsig[i] = r;
+  }
+}
+
+__global__ void BGV_BULK k_sig_fix(dev_batch b, dev_work w) {
+  const uint32_t i = gtid();
+  if (i >= b.n_sets) return;
+  if (w.sig_code[i] == C_OK && !w.sig_grp[i]) {
+    w.sig_code[i] = C_POINT_NOT_IN_GROUP;
+    g2a z;
+    z.x = fp2_zero();
+    z.y = fp2_zero();
+    w.sig_aff[i] = z;
+  }
+}
+
+// latency mode: lane t maps u_(t & 1) of message t >> 1; then one lane per
+// message adds the two points and clears the cofactor
+__global__ void __launch_bounds__(64, BGV_HASH_WAVES) k_hash_map(dev_batch b, dev_work w) {
+  const uint32_t t = gtid();
+  if (t >= 2u * b.n_sets) return;
+  const uint32_t i = t >> 1;
+  uint8_t m[32];
+#pragma unroll
+  for (int k = 0; k < 32; k++) m[k] = b.msgs[32u * i + k];
+  g2j q;
+  hash_to_g2_map(q, m, t & 1u);
+  w.q_part[t] = q;
+}
+
+__global__ void __launch_bounds__(64, BGV_HASH_WAVES) k_hash_clear(dev_batch b, dev_work w) {
+  const uint32_t i = gtid();
+  if (i >= b.n_sets) return;
+  g2j h;
+  hash_to_g2_finish(h, w.q_part[2u * i], w.q_part[2u * i + 1u]);
+  g2a ha;
+  jac_to_aff(ha, h);
+  w.h_aff[i] = ha;
+}
+
 // ----------------------------------------------------------------- k_hash
 __global__ void __launch_bounds__(64, BGV_HASH_WAVES) k_hash(dev_batch b, dev_work w) {
   const uint32_t i = gtid();
@@ -735,13 +820,29 @@ void launch_prep(hipStream_t st, const dev_batch& b, const dev_work& w) {
 void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work& w) {
   const uint32_t span = 1u << b.span_log2;
   switch (stage) {
-    case ST_SIG: BGV_LAUNCH(k_sig, b.n_sets, b, w); break;
-    case ST_HASH: BGV_LAUNCH(k_hash, b.n_sets, b, w); break;
+    case ST_SIG:
+      if (b.split && !b.msm) {
+        BGV_LAUNCH(k_sig_dec, b.n_sets, b, w);
+        if (b.n_sets) hipLaunchKernelGGL(k_sig_split, dim3(2u * ((b.n_sets + 63u) / 64u)), dim3(64), 0, st, b, w);
+        BGV_LAUNCH(k_sig_fix, b.n_sets, b, w);
+      } else {
+        BGV_LAUNCH(k_sig, b.n_sets, b, w);
+      }
+      break;
+    case ST_HASH:
+      if (b.split) {
+        BGV_LAUNCH(k_hash_map, 2u * b.n_sets, b, w);
+        BGV_LAUNCH(k_hash_clear, b.n_sets, b, w);
+      } else {
+        BGV_LAUNCH(k_hash, b.n_sets, b, w);
+      }
+      break;
     case ST_PK:  // after launch_prep
       BGV_LAUNCH(k_pk_chunk, b.chunk_bound, b, w);
       BGV_LAUNCH(k_pk, b.n_sets, b, w);
       break;
     case ST_SIG_SCALE:
+      if (b.split && !b.msm) break;  // [r_i] sigma_i already ran in k_sig_split
       if (b.msm) {
         BGV_LAUNCH(k_msm_bucket, b.n_jobs * 16u, b, w);
         BGV_LAUNCH(k_msm_window, b.n_jobs * 16u, b, w);

@@ -233,6 +233,23 @@ BGV_NIH void iso_map_g2(g2j& r, const g2a& p) {
   fp2_mul(r.y, t, p.y);
 }
 
+// split form for small batches (two lanes per message): lane k in {0, 1}
+// maps u_k through SSWU and the isogeny; hash_to_g2_finish adds the two
+// points and clears the cofactor.  Same values as hash_to_g2.
+BGV_NI void hash_to_g2_map(g2j& out, const uint8_t msg[32], uint32_t k) {
+  fp2_t u0, u1;
+  hash_to_field_fp2x2(u0, u1, msg);
+  g2a qa;
+  map_to_curve_sswu(qa, k ? u1 : u0);
+  iso_map_g2(out, qa);
+}
+
+BGV_NI void hash_to_g2_finish(g2j& out, const g2j& q0, const g2j& q1) {
+  g2j r;
+  jac_add(r, q0, q1);
+  g2_clear_cofactor(out, r);
+}
+
 // full hash_to_G2(msg[32]) -> Jacobian point in G2
 BGV_NI void hash_to_g2(g2j& out, const uint8_t msg[32]) {
   fp2_t u0, u1;

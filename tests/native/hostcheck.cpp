@@ -163,4 +163,13 @@ extern "C" {
 void hc_chacha20_block(const uint32_t* key, uint32_t counter, const uint32_t* nonce, uint32_t* out) {
   chacha20_block(out, key, counter, nonce);
 }
+// split hash_to_G2 (two map lanes + finish) equals the one-lane hash_to_g2
+int hc_hash_to_g2_split_eq(const uint8_t* msg) {
+  g2j a, b, q0, q1;
+  hash_to_g2(a, msg);
+  hash_to_g2_map(q0, msg, 0);
+  hash_to_g2_map(q1, msg, 1);
+  hash_to_g2_finish(b, q0, q1);
+  return jac_eq(a, b) ? 1 : 0;
+}
 }

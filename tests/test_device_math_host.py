@@ -278,3 +278,10 @@ def test_chacha20_block_rfc8439():
     lib.hc_chacha20_block(key, 1, nonce, out)
     assert list(out) == [0xE4E7F110, 0x15593BD1, 0x1FDD0F50, 0xC47120A3, 0xC7F4D1C7, 0x0368C033, 0x9AAA2204, 0x4E6CD4C3,
                          0x466482D2, 0x09AA9F07, 0x05D7C214, 0xA2028BD9, 0xD19C12B5, 0xB94E16DE, 0xE883D0CB, 0x4E3C50A2]
+
+
+def test_hash_to_g2_split_equals_single_lane():
+    """latency mode (k_hash_map + k_hash_clear) computes the same H(m)"""
+    for k in range(8):
+        msg = bytes((k * 37 + i) & 0xFF for i in range(32))
+        assert lib.hc_hash_to_g2_split_eq(msg) == 1

@@ -328,3 +328,33 @@ def test_signature_msm_bit_identical_to_per_set_scaling(monkeypatch):
         finally:
             d.close()
     assert outs["0"] == outs["1"]
+
+
+@pytest.mark.gpu
+def test_latency_split_mode_bit_identical(monkeypatch):
+    """Latency mode (BGV_SPLIT=1, default below 65,536 sets: two map lanes
+    per message, subgroup check beside [r_i] sigma_i) and the one-lane-per-set
+    kernels (BGV_SPLIT=0) give the same batch partial, byte for byte, and the
+    same per-job verdicts and set codes on the golden jobs (which include
+    off-curve and out-of-subgroup signatures)."""
+    from lodestar_amd import native
+    outs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("BGV_SPLIT", mode)
+        d = native.Device(0)
+        try:
+            d.pubkeys_set(0, G.interop_pubkeys48(), native.PK_COMPRESSED_48)
+            a, expected, codes = G.golden_arrays([0, 1, 9, 11, 12, 13], scalars_seed=3)
+            part, _, ok = d.partial(a)
+            ga, gexp, gcodes = G.golden_arrays(scalars_seed=3)
+            jr, sc = d.verify(ga)
+            d.gen_keys(1000, 256, 5)
+            syn, bad = _synthetic_on(d, 200, 8, 1000, 256, 9, fault_every=17)
+            jr2, _ = d.verify(syn)
+            outs[mode] = (part, ok, jr.tolist(), sc.tolist(), jr2.tolist(), bad)
+        finally:
+            d.close()
+    assert outs["0"][0] == outs["1"][0]
+    assert outs["0"][1:5] == outs["1"][1:5]
+    assert outs["1"][2] == gexp and outs["1"][3] == gcodes
+    assert outs["1"][4] == np.where(outs["1"][5], 0, 1).tolist()
