@@ -536,11 +536,12 @@ __global__ void BGV_BULK k_item_job(dev_batch b, dev_work w) {
 // k_miller (the set-pair Miller loops) lives in bgv_miller.hip: that unit
 // uses the Fp2 product leaf with lazy reduction (fp2.h BGV_FP2_LEAF).
 
-// Cooperative variant (miller_coop.h): 10 pairs per 64-lane workgroup, six
-// lanes per pair, pair t < n_sets is (r_t PK_t, H(m_t)), then (-G1, S_job).
+// Cooperative variant (miller_coop.h): COOP_GROUPS pairs per 64-lane
+// workgroup, 6 x COOP_SUB lanes per pair, pair t < n_sets is (r_t PK_t, H(m_t)), then (-G1, S_job).
 __global__ void __launch_bounds__(64, BGV_WAVES) k_miller_coop(dev_batch b, dev_work w, uint32_t first, uint32_t count) {
   __shared__ coop_grp sm[COOP_GROUPS];
-  const uint32_t lane = threadIdx.x, grp = lane / COOP_LANES, k = lane % COOP_LANES;
+  const uint32_t lane = threadIdx.x, grp = lane / COOP_GROUP_LANES;
+  const uint32_t k = (lane % COOP_GROUP_LANES) / COOP_SUB, q = lane % COOP_SUB;
   const uint32_t t = first + blockIdx.x * COOP_GROUPS + grp;
   const bool in_range = grp < COOP_GROUPS && t < first + count;
   bool active = in_range;
@@ -561,7 +562,7 @@ __global__ void __launch_bounds__(64, BGV_WAVES) k_miller_coop(dev_batch b, dev_
       P.y = G1_NEG_Y_MONT;
       Q = w.s_aff[j];
     }
-    if (active && k == 0) {
+    if (active && k == 0 && q == 0) {
       coop_grp& g = sm[grp];
       g.T[0] = Q.x;
       g.T[1] = Q.y;
@@ -575,8 +576,8 @@ __global__ void __launch_bounds__(64, BGV_WAVES) k_miller_coop(dev_batch b, dev_
     }
   }
   __syncthreads();
-  coop_miller(sm[grp < COOP_GROUPS ? grp : 0], k, active);
-  if (in_range) {
+  coop_miller(sm[grp < COOP_GROUPS ? grp : 0], k, q, active);
+  if (in_range && q == 0) {
     fp2_t v;
     if (active) v = sm[grp].f[k];
     else v = k == 0 ? fp2_one() : fp2_zero();  // skipped pair contributes 1

@@ -25,8 +25,17 @@
 
 namespace bgv {
 
+// BGV_COOP_SUB = 3: every coefficient lane k is three sub-lanes q, one per
+// Karatsuba Fp product of each Fp2 product (coop_prod_sub), so a product
+// round costs the latency of ONE Fp product instead of three.  18 lanes per
+// pair, 3 pairs per wave.  BGV_COOP_SUB = 1: the six-lane form.
+#ifndef BGV_COOP_SUB
+#define BGV_COOP_SUB 3
+#endif
 constexpr int COOP_LANES = 6;
-constexpr int COOP_GROUPS = 10;  // 60 of the 64 lanes of a wave
+constexpr int COOP_SUB = BGV_COOP_SUB;
+constexpr int COOP_GROUP_LANES = COOP_LANES * COOP_SUB;
+constexpr int COOP_GROUPS = 64 / COOP_GROUP_LANES;  // 10 (60 of 64 lanes) or 3 (54)
 
 struct coop_grp {
   fp2_t f[6];     // w-basis coefficients of the accumulator
@@ -36,6 +45,9 @@ struct coop_grp {
   fp2_t line[3];  // a0, a1, b1
   fp2_t r[8];     // per-round products
   fp2_t a[6];     // per-lane staged operand
+#if BGV_COOP_SUB == 3
+  fp_t P[6][3];   // sub-lane Fp products of coefficient lane k
+#endif
 };
 
 // f^2 by the symmetric schoolbook in the w-basis: lane k sums 4 products
@@ -71,16 +83,60 @@ __device__ __noinline__ void coop_prod(const fp2_t* a, const fp2_t* b, fp2_t* ou
   *out = r;
 }
 
+// LDS hand-off between the sub-lanes of one coefficient lane (same wave):
+// wait for this wave's LDS writes, and keep the compiler from moving memory
+// accesses across
+__device__ __forceinline__ void coop_wave_sync() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// *out = *a * *b over the three sub-lanes q of lane k: q0 a0 b0, q1 a1 b1,
+// q2 (a0 + a1)(b0 + b1) (one leaf call on every lane), then q0 / q1 form
+// c0 = P0 - P1 / c1 = P2 - P0 - P1.  All three sub-lanes of k call it
+// together (the branch conditions around every call depend on k only).
+__device__ __forceinline__ void coop_prod_sub(fp_t* P, uint32_t q, const fp2_t* a, const fp2_t* b, fp2_t* out) {
+  fp_t u, v;
+  if (q == 0) {
+    u = a->c0;
+    v = b->c0;
+  } else if (q == 1) {
+    u = a->c1;
+    v = b->c1;
+  } else {
+    fp_add_lazy(u, a->c0, a->c1);  // < 2p, product inputs only
+    fp_add_lazy(v, b->c0, b->c1);
+  }
+  fp_t r;
+  fp_mul(r, u, v);
+  P[q] = r;
+  coop_wave_sync();
+  if (q == 0) {
+    fp_t t;
+    fp_sub(t, P[0], P[1]);
+    out->c0 = t;
+  } else if (q == 1) {
+    fp_t t, w;
+    fp_add(w, P[0], P[1]);
+    fp_sub(t, P[2], w);
+    out->c1 = t;
+  }
+  coop_wave_sync();
+}
+
+#if BGV_COOP_SUB == 3
+#define COOP_PROD(pa, pb, out) coop_prod_sub(g.P[k], q, (pa), (pb), (out))
+#else
+#define COOP_PROD(pa, pb, out) coop_prod((pa), (pb), (out))
+#endif
+
 // lanes 0..5: g.r[k] <- c_k of f * (a0 + a1 w^2 + b1 w^3); then f <- that
-__device__ __forceinline__ void coop_line_round(coop_grp& g, uint32_t k, bool active) {
+__device__ __forceinline__ void coop_line_round(coop_grp& g, uint32_t k, uint32_t q, bool active) {
   fp2_t acc;
   if (active) {
-    coop_prod(&g.f[k], &g.line[0], &g.r[k]);
+    COOP_PROD(&g.f[k], &g.line[0], &g.r[k]);
     acc = g.r[k];
 #pragma unroll 1
     for (uint32_t s = 0; s < 2; s++) {
       const uint32_t sh = s ? 3u : 2u;  // w^2 (a1) and w^3 (b1)
-      coop_prod(&g.f[(k + 6 - sh) % 6], &g.line[1 + s], &g.a[k]);
+      COOP_PROD(&g.f[(k + 6 - sh) % 6], &g.line[1 + s], &g.a[k]);
       fp2_t t = g.a[k];
       if (k < sh) fp2_mul_xi(t, t);
       fp2_add(acc, acc, t);
@@ -94,7 +150,7 @@ __device__ __forceinline__ void coop_line_round(coop_grp& g, uint32_t k, bool ac
 // Miller loop of the pair held in g (T := Q, P in px/py) by lanes k = 0..5.
 // Every lane of the workgroup calls it (barriers inside); lanes outside a
 // pair, or of a skipped pair, pass active = false.
-__device__ void coop_miller(coop_grp& g, uint32_t k, bool active) {
+__device__ void coop_miller(coop_grp& g, uint32_t k, uint32_t q, bool active) {
   for (int b = 62; b >= 0; b--) {
     // ---- S: f <- f^2 (not on the first iteration: f = 1)
     if (b != 62) {
@@ -103,7 +159,7 @@ __device__ void coop_miller(coop_grp& g, uint32_t k, bool active) {
 #pragma unroll 1
         for (int p = 0; p < 4; p++) {
           const sq_term e = SQ_TAB[k][p];
-          coop_prod(&g.f[e.i], &g.f[e.j], &g.a[k]);
+          COOP_PROD(&g.f[e.i], &g.f[e.j], &g.a[k]);
           fp2_t t = g.a[k];
           if (e.dbl) fp2_dbl(t, t);
           if (e.xi) fp2_mul_xi(t, t);
@@ -125,7 +181,7 @@ __device__ void coop_miller(coop_grp& g, uint32_t k, bool active) {
         fp2_add(g.a[k], g.T[1], g.T[2]);
         pa = pb = &g.a[k];
       } else if (k == 4) pb = &g.T[0];
-      coop_prod(pa, pb, &g.r[k]);
+      COOP_PROD(pa, pb, &g.r[k]);
     }
     __syncthreads();
     // ---- D2: the rest of miller_dbl_step (same formulas):
@@ -153,7 +209,7 @@ __device__ void coop_miller(coop_grp& g, uint32_t k, bool active) {
       else { g.a[k] = H; pb = &g.py; }
       if (k == 1) fp2_sub(mine, E, B);  // a0
       __syncthreads();                   // r[0..4] fully read before r[5..] / r[k] writes
-      coop_prod(pa, pb, &g.r[k == 0 ? 0 : k + 2]);
+      COOP_PROD(pa, pb, &g.r[k == 0 ? 0 : k + 2]);
     } else {
       __syncthreads();
     }
@@ -179,12 +235,12 @@ __device__ void coop_miller(coop_grp& g, uint32_t k, bool active) {
       }
       __syncthreads();
     } else {
-      coop_line_round(g, k, active);
+      coop_line_round(g, k, q, active);
     }
     if (!((BLS_X_ABS >> b) & 1ull)) continue;
     // ---- addition step (miller_add_step)
     //   R1  k0: yQ Z  k1: xQ Z                               -> r0, r1
-    if (active && k < 2) coop_prod(k ? &g.Q[0] : &g.Q[1], &g.T[2], &g.r[k]);
+    if (active && k < 2) COOP_PROD(k ? &g.Q[0] : &g.Q[1], &g.T[2], &g.r[k]);
     __syncthreads();
     //   th = Y - yQ Z (-> r6), la = X - xQ Z (-> r7)
     //   R2  k0: th xQ  k1: la yQ  k2: th xP  k3: la yP  k4: th^2 = C  k5: la^2 = D
@@ -199,7 +255,7 @@ __device__ void coop_miller(coop_grp& g, uint32_t k, bool active) {
       else if (k == 2) pb = &g.px;
       else if (k == 3) pb = &g.py;
       __syncthreads();  // r0, r1 read by every lane before r[k] is overwritten
-      coop_prod(&g.a[k], pb, &g.r[k]);
+      COOP_PROD(&g.a[k], pb, &g.r[k]);
       if (k == 0) g.r[6] = th;
       if (k == 1) g.r[7] = la;
     } else {
@@ -213,7 +269,7 @@ __device__ void coop_miller(coop_grp& g, uint32_t k, bool active) {
       const fp2_t* pb = &g.r[7];
       if (k == 1) { pa = &g.T[2]; pb = &g.r[4]; }
       else if (k == 2) { pa = &g.T[0]; pb = &g.r[5]; }
-      coop_prod(pa, pb, &g.a[k]);
+      COOP_PROD(pa, pb, &g.a[k]);
     }
     if (active && k == 3) {
       fp2_sub(g.line[0], g.r[0], g.r[1]);
@@ -239,7 +295,7 @@ __device__ void coop_miller(coop_grp& g, uint32_t k, bool active) {
       __syncthreads();  // a[0..2] read by every lane before being restaged
       g.a[k] = opd;
       pa = &g.a[k];
-      coop_prod(pa, pb, &g.r[k]);
+      COOP_PROD(pa, pb, &g.r[k]);
     } else {
       __syncthreads();
     }
@@ -250,7 +306,7 @@ __device__ void coop_miller(coop_grp& g, uint32_t k, bool active) {
       g.T[2] = g.r[3];
     }
     __syncthreads();
-    coop_line_round(g, k, active);
+    coop_line_round(g, k, q, active);
   }
   // x < 0: conjugate (negate the odd powers of w)
   if (active && (k & 1)) fp2_neg(g.f[k], g.f[k]);
