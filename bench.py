@@ -10,7 +10,8 @@ table resident in HBM.  One block = one verifySignatureSets call = one job
 A step = one pass of the hot path over the whole segment: every set's
 signature decoded + subgroup-checked, every message hashed to G2, every
 pubkey set gathered and aggregated from the table, 64-bit random scalars
-drawn (getrandom) and applied, one Miller loop per set, per-block products,
+drawn (device ChaCha20 keyed by getrandom) and applied, one Miller loop per
+set, per-block products,
 and the final exponentiation (one for the segment; per-block ones only if
 it fails).  Inputs (indices, messages, signatures) are resident in HBM
 before the timed region.  Multi-GPU (weak scaling): every rank verifies its
@@ -238,7 +239,7 @@ def main():
     d.gen_sign(darr, sigs, on_device=True)
     darr["sigs"] = sigs
     darr["sig_len"] = torch.full((n_sets,), 96, dtype=torch.int32, device=dev)
-    darr["scalars"] = None  # drawn by the library per call (getrandom)
+    darr["scalars"] = None  # drawn by the library per call (device ChaCha20 keyed by getrandom)
     log(f"[bench] rank {rank}: {n_sets} sets signed in {time.time() - t0:.1f}s")
 
     def step():

@@ -869,7 +869,7 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       launch_miller(st, b, w);  // bgv_miller.hip
       break;
     case ST_MILLER_JOBS:  // (-G1, S_job) pairs: needs ST_S_TREE
-      // always the six-lane loop: one pair per job is latency-bound (a lone
+      // always the cooperative loop: one pair per job is latency-bound (a lone
       // lane takes ~19 ms at C4, the cooperative loop ~5 ms) and its waves
       // fit on the SIMDs the set-pair kernel leaves free
       if (b.n_jobs)

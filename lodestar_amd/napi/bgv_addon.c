@@ -262,7 +262,7 @@ static int read_batch(napi_env env, napi_value obj, verify_job* j, int pin) {
   j->b.sig_len = (const uint32_t*)p[F_LEN];
   j->b.raw_pks = (const uint8_t*)p[F_RAW];
   j->b.n_raw = (uint32_t)(n[F_RAW] / 96);
-  j->b.scalars = NULL; /* getrandom() inside the library */
+  j->b.scalars = NULL; /* drawn inside the library (device ChaCha20 keyed by getrandom) */
   j->b.on_device = 0;
   return 0;
 }

@@ -393,7 +393,7 @@ class BlsGpuVerifier:
     # -- device -------------------------------------------------------------
     def _scalars(self, n: int) -> np.ndarray | None:
         if self._rng is None:
-            return None  # getrandom() inside the library
+            return None  # drawn inside the library (device ChaCha20 keyed by getrandom)
         s = self._rng.integers(1, 2**64 - 1, size=max(n, 1), dtype=np.uint64, endpoint=True)
         return s
 

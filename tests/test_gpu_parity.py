@@ -66,7 +66,7 @@ def test_verdict_independent_of_scalars(dev):
         jr, _ = dev.verify(arrays)
         assert jr.tolist() == expected
     arrays, expected, _ = G.golden_arrays()
-    arrays["scalars"] = None  # getrandom() inside the library
+    arrays["scalars"] = None  # drawn inside the library (device ChaCha20 keyed by getrandom)
     jr, _ = dev.verify(arrays)
     assert jr.tolist() == expected
 
@@ -186,7 +186,7 @@ def test_microbench_runs(dev):
 
 
 def test_cooperative_miller_bit_identical_to_serial(monkeypatch):
-    """The six-lane cooperative Miller loop (miller_coop.h, default) and the
+    """The cooperative Miller loop (miller_coop.h, default, 18 lanes per pair) and the
     one-lane loop (pairing.h, BGV_MILLER=serial) produce the same Fp12 batch
     partial, byte for byte, and the same verdicts."""
     from lodestar_amd import native
