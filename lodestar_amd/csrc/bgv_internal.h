@@ -90,6 +90,8 @@ void launch_pk_validate(hipStream_t st, const uint8_t* in, uint32_t n, int32_t* 
 void launch_prep(hipStream_t st, const dev_batch& b, const dev_work& w);  // before ST_PK / ST_MILLER
 void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work& w);
 void launch_miller(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_miller.hip
+void launch_sig_split_coop(hipStream_t st, const dev_batch& b, const dev_work& w);   // bgv_latency.hip
+void launch_hash_clear_coop(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_latency.hip
 void launch_fp12_tail(hipStream_t st, int stage, const dev_batch& b, const dev_work& w);  // bgv_tail.hip
 void launch_combine_final(hipStream_t st, const fp12_t* parts, uint32_t n, uint32_t* flag);
 void launch_fp12_convert(hipStream_t st, const fp12_t* in, fp12_t* out, uint32_t n, bool to_mont);

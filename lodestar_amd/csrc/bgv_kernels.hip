@@ -50,7 +50,6 @@
 #endif
 #include "bgv_internal.h"
 #include "miller_coop.h"
-#include "coop_g2.h"
 
 namespace bgv {
 
@@ -222,51 +221,13 @@ __global__ void BGV_BULK k_sig_fix(dev_batch b, dev_work w) {
   }
 }
 
-// Latency mode with cooperative G2 arithmetic (coop_g2.h, BGV_COOP_G2):
-// nine lanes per point, seven points per wave.  Lane 63 and groups past
-// n_sets run on a copy of set 0 into their own scratch and write nothing.
+// The cooperative G2 kernels of the latency mode (k_sig_split_coop,
+// k_hash_clear_coop) live in bgv_latency.hip: they run at 1 wave/SIMD, and
+// sharing this unit's non-inlined curve helpers with them raised k_sig to
+// 321 VGPRs (1 wave/SIMD; C4 sig decode 6 -> 21 ms).
 #ifndef BGV_COOP_G2
 #define BGV_COOP_G2 1
 #endif
-__global__ void __launch_bounds__(64, 1) k_sig_split_coop(dev_batch b, dev_work w) {
-  __shared__ cg_scratch sm[CG_GROUPS + 1];
-  __shared__ g2j tabs[CG_GROUPS + 1][16];
-  const uint32_t nbg = (b.n_sets + CG_GROUPS - 1) / CG_GROUPS;
-  const bool check = blockIdx.x < nbg;
-  const uint32_t lane = threadIdx.x, grp = lane / CG_LANES, r9 = lane % CG_LANES, s = r9 / 3, q = r9 % 3;
-  const uint32_t i0 = (check ? blockIdx.x : blockIdx.x - nbg) * CG_GROUPS + grp;
-  const bool own = grp < CG_GROUPS && i0 < b.n_sets;
-  const uint32_t i = own ? i0 : 0u;
-  const bool lead = own && s == 0 && q == 0;
-  const bool live = w.sig_code[i] == C_OK && !w.sig_inf[i];  // decode outcome (k_sig_dec)
-  g2j p;
-  jac_from_aff(p, w.sig_aff[i]);
-  if (check) {
-    const bool ok = !live || cg_in_subgroup(&sm[grp], s, q, p);
-    if (lead) w.sig_grp[i] = ok ? 1u : 0u;
-  } else {
-    g2j r;
-    if (live) cg_mul_u64_w4(&sm[grp], tabs[grp], s, q, r, p, b.scalars[i]);
-    else jac_set_inf(r);  // infinity signature: blst skips it (adds the identity)
-    if (lead) w.rsig[i] = r;
-  }
-}
-
-__global__ void __launch_bounds__(64, 1) k_hash_clear_coop(dev_batch b, dev_work w) {
-  __shared__ cg_scratch sm[CG_GROUPS + 1];
-  const uint32_t lane = threadIdx.x, grp = lane / CG_LANES, r9 = lane % CG_LANES, s = r9 / 3, q = r9 % 3;
-  const uint32_t i0 = blockIdx.x * CG_GROUPS + grp;
-  const bool own = grp < CG_GROUPS && i0 < b.n_sets;
-  const uint32_t i = own ? i0 : 0u;
-  g2j r, h;
-  cg_add(&sm[grp], s, q, r, w.q_part[2u * i], w.q_part[2u * i + 1u]);
-  cg_clear_cofactor(&sm[grp], s, q, h, r);
-  if (own && s == 0 && q == 0) {
-    g2a ha;
-    jac_to_aff(ha, h);
-    w.h_aff[i] = ha;
-  }
-}
 
 // latency mode: lane t maps u_(t & 1) of message t >> 1; then one lane per
 // message adds the two points and clears the cofactor
@@ -873,7 +834,7 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
         BGV_LAUNCH(k_sig_dec, b.n_sets, b, w);
         if (b.n_sets) {
           if (BGV_COOP_G2)
-            hipLaunchKernelGGL(k_sig_split_coop, dim3(2u * ((b.n_sets + CG_GROUPS - 1) / CG_GROUPS)), dim3(64), 0, st, b, w);
+            launch_sig_split_coop(st, b, w);  // bgv_latency.hip
           else
             hipLaunchKernelGGL(k_sig_split, dim3(2u * ((b.n_sets + 63u) / 64u)), dim3(64), 0, st, b, w);
         }
@@ -886,7 +847,7 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       if (b.split) {
         BGV_LAUNCH(k_hash_map, 2u * b.n_sets, b, w);
         if (BGV_COOP_G2) {
-          if (b.n_sets) hipLaunchKernelGGL(k_hash_clear_coop, dim3((b.n_sets + CG_GROUPS - 1) / CG_GROUPS), dim3(64), 0, st, b, w);
+          launch_hash_clear_coop(st, b, w);  // bgv_latency.hip
         } else {
           BGV_LAUNCH(k_hash_clear, b.n_sets, b, w);
         }
