@@ -549,7 +549,8 @@ __global__ void BGV_BULK k_item_job(dev_batch b, dev_work w) {
 __global__ void __launch_bounds__(64, BGV_WAVES) k_miller_coop(dev_batch b, dev_work w, uint32_t first, uint32_t count) {
   __shared__ coop_grp sm[COOP_GROUPS];
   const uint32_t lane = threadIdx.x, grp = lane / COOP_GROUP_LANES;
-  const uint32_t k = (lane % COOP_GROUP_LANES) / COOP_SUB, q = lane % COOP_SUB;
+  const uint32_t r = lane % COOP_GROUP_LANES;
+  const uint32_t k = r / (COOP_SUB * COOP_HALF), h = (r / COOP_SUB) % COOP_HALF, q = r % COOP_SUB;
   const uint32_t t = first + blockIdx.x * COOP_GROUPS + grp;
   const bool in_range = grp < COOP_GROUPS && t < first + count;
   bool active = in_range;
@@ -570,7 +571,7 @@ __global__ void __launch_bounds__(64, BGV_WAVES) k_miller_coop(dev_batch b, dev_
       P.y = G1_NEG_Y_MONT;
       Q = w.s_aff[j];
     }
-    if (active && k == 0 && q == 0) {
+    if (active && k == 0 && q == 0 && h == 0) {
       coop_grp& g = sm[grp];
       g.T[0] = Q.x;
       g.T[1] = Q.y;
@@ -584,8 +585,8 @@ __global__ void __launch_bounds__(64, BGV_WAVES) k_miller_coop(dev_batch b, dev_
     }
   }
   __syncthreads();
-  coop_miller(sm[grp < COOP_GROUPS ? grp : 0], k, q, active);
-  if (in_range && q == 0) {
+  coop_miller(sm[grp < COOP_GROUPS ? grp : 0], k, h, q, active);
+  if (in_range && q == 0 && h == 0) {
     fp2_t v;
     if (active) v = sm[grp].f[k];
     else v = k == 0 ? fp2_one() : fp2_zero();  // skipped pair contributes 1

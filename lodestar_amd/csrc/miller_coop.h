@@ -32,10 +32,18 @@ namespace bgv {
 #ifndef BGV_COOP_SUB
 #define BGV_COOP_SUB 3
 #endif
+// BGV_COOP_HALF = 2 (with COOP_SUB = 3): every coefficient lane is also split
+// in two halves h that share the squaring's four products and the line
+// multiplication's three (2 + 2 and 2 + 1 per half), so those steps take 2
+// product rounds instead of 4 and 3.  36 lanes per pair, one pair per wave.
+#ifndef BGV_COOP_HALF
+#define BGV_COOP_HALF 2
+#endif
 constexpr int COOP_LANES = 6;
 constexpr int COOP_SUB = BGV_COOP_SUB;
-constexpr int COOP_GROUP_LANES = COOP_LANES * COOP_SUB;
-constexpr int COOP_GROUPS = 64 / COOP_GROUP_LANES;  // 10 (60 of 64 lanes) or 3 (54)
+constexpr int COOP_HALF = (BGV_COOP_SUB == 3) ? BGV_COOP_HALF : 1;
+constexpr int COOP_GROUP_LANES = COOP_LANES * COOP_SUB * COOP_HALF;
+constexpr int COOP_GROUPS = 64 / COOP_GROUP_LANES;  // 10 (60 of 64 lanes), 3 (54) or 1 (36)
 
 struct coop_grp {
   fp2_t f[6];     // w-basis coefficients of the accumulator
@@ -46,7 +54,11 @@ struct coop_grp {
   fp2_t r[8];     // per-round products
   fp2_t a[6];     // per-lane staged operand
 #if BGV_COOP_SUB == 3
-  fp_t P[6][3];   // sub-lane Fp products of coefficient lane k
+  fp_t P[6 * COOP_HALF][3];  // sub-lane Fp products of coefficient lane (k, h)
+#endif
+#if BGV_COOP_SUB == 3 && BGV_COOP_HALF == 2
+  fp2_t hs[6][2];  // per-half partial sums
+  fp2_t ah[6][2];  // per-half staged products
 #endif
 };
 
@@ -122,14 +134,38 @@ __device__ __forceinline__ void coop_prod_sub(fp_t* P, uint32_t q, const fp2_t* 
 }
 
 #if BGV_COOP_SUB == 3
-#define COOP_PROD(pa, pb, out) coop_prod_sub(g.P[k], q, (pa), (pb), (out))
+#define COOP_PROD(pa, pb, out) coop_prod_sub(g.P[k * COOP_HALF + h], q, (pa), (pb), (out))
 #else
 #define COOP_PROD(pa, pb, out) coop_prod((pa), (pb), (out))
 #endif
 
 // lanes 0..5: g.r[k] <- c_k of f * (a0 + a1 w^2 + b1 w^3); then f <- that
-__device__ __forceinline__ void coop_line_round(coop_grp& g, uint32_t k, uint32_t q, bool active) {
+__device__ __forceinline__ void coop_line_round(coop_grp& g, uint32_t k, uint32_t h, uint32_t q, bool active) {
   fp2_t acc;
+#if BGV_COOP_SUB == 3 && BGV_COOP_HALF == 2
+  // half 0: f_k a0 and the w^2 term; half 1: the w^3 term (same sum order)
+  if (active) {
+    if (h == 0) {
+      COOP_PROD(&g.f[k], &g.line[0], &g.r[k]);
+      acc = g.r[k];
+      COOP_PROD(&g.f[(k + 4) % 6], &g.line[1], &g.ah[k][0]);
+      fp2_t t = g.ah[k][0];
+      if (k < 2) fp2_mul_xi(t, t);
+      fp2_add(acc, acc, t);
+    } else {
+      COOP_PROD(&g.f[(k + 3) % 6], &g.line[2], &g.ah[k][1]);
+      acc = g.ah[k][1];
+      if (k < 3) fp2_mul_xi(acc, acc);
+    }
+    g.hs[k][h] = acc;
+    coop_wave_sync();
+    fp2_add(acc, g.hs[k][0], g.hs[k][1]);
+  }
+  __syncthreads();
+  if (active) g.f[k] = acc;
+  __syncthreads();
+  return;
+#endif
   if (active) {
     COOP_PROD(&g.f[k], &g.line[0], &g.r[k]);
     acc = g.r[k];
@@ -150,12 +186,27 @@ __device__ __forceinline__ void coop_line_round(coop_grp& g, uint32_t k, uint32_
 // Miller loop of the pair held in g (T := Q, P in px/py) by lanes k = 0..5.
 // Every lane of the workgroup calls it (barriers inside); lanes outside a
 // pair, or of a skipped pair, pass active = false.
-__device__ void coop_miller(coop_grp& g, uint32_t k, uint32_t q, bool active) {
+__device__ void coop_miller(coop_grp& g, uint32_t k, uint32_t h, uint32_t q, bool active) {
   for (int b = 62; b >= 0; b--) {
     // ---- S: f <- f^2 (not on the first iteration: f = 1)
     if (b != 62) {
       fp2_t acc = fp2_zero();
       if (active) {
+#if BGV_COOP_SUB == 3 && BGV_COOP_HALF == 2
+        // half h: products 2h, 2h + 1 of lane k; (t0 + t1) + (t2 + t3)
+#pragma unroll 1
+        for (int p = 2 * (int)h; p < 2 * (int)h + 2; p++) {
+          const sq_term e = SQ_TAB[k][p];
+          COOP_PROD(&g.f[e.i], &g.f[e.j], &g.ah[k][h]);
+          fp2_t t = g.ah[k][h];
+          if (e.dbl) fp2_dbl(t, t);
+          if (e.xi) fp2_mul_xi(t, t);
+          if (e.use) fp2_add(acc, acc, t);
+        }
+        g.hs[k][h] = acc;
+        coop_wave_sync();
+        fp2_add(acc, g.hs[k][0], g.hs[k][1]);
+#else
 #pragma unroll 1
         for (int p = 0; p < 4; p++) {
           const sq_term e = SQ_TAB[k][p];
@@ -165,6 +216,7 @@ __device__ void coop_miller(coop_grp& g, uint32_t k, uint32_t q, bool active) {
           if (e.xi) fp2_mul_xi(t, t);
           if (e.use) fp2_add(acc, acc, t);
         }
+#endif
       }
       __syncthreads();
       if (active) g.f[k] = acc;
@@ -235,7 +287,7 @@ __device__ void coop_miller(coop_grp& g, uint32_t k, uint32_t q, bool active) {
       }
       __syncthreads();
     } else {
-      coop_line_round(g, k, q, active);
+      coop_line_round(g, k, h, q, active);
     }
     if (!((BLS_X_ABS >> b) & 1ull)) continue;
     // ---- addition step (miller_add_step)
@@ -306,7 +358,7 @@ __device__ void coop_miller(coop_grp& g, uint32_t k, uint32_t q, bool active) {
       g.T[2] = g.r[3];
     }
     __syncthreads();
-    coop_line_round(g, k, q, active);
+    coop_line_round(g, k, h, q, active);
   }
   // x < 0: conjugate (negate the odd powers of w)
   if (active && (k & 1)) fp2_neg(g.f[k], g.f[k]);
