@@ -352,7 +352,7 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, std::vector<uin
   // latency mode below one chip-full of lanes: hash maps on two lanes per
   // set, subgroup check beside the signature scaling (bgv_kernels.hip)
   d.split = c->split >= 0 ? (uint32_t)c->split : (n < 65536 ? 1u : 0u);
-  // cooperative Miller loop (18 lanes per pair, low latency) unless the batch alone
+  // cooperative Miller loop (36 lanes per pair, low latency) unless the batch alone
   // fills the GPU, where the one-lane loop does less work per pair
   d.miller_coop = c->miller_mode >= 0 ? (uint32_t)c->miller_mode : (n < 65536 ? 1u : 0u);
   // sum r_i sigma_i per job by a bucket MSM (16 x 4-bit windows, ~1,800 G2

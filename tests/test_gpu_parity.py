@@ -186,7 +186,7 @@ def test_microbench_runs(dev):
 
 
 def test_cooperative_miller_bit_identical_to_serial(monkeypatch):
-    """The cooperative Miller loop (miller_coop.h, default, 18 lanes per pair) and the
+    """The cooperative Miller loop (miller_coop.h, default, 36 lanes per pair) and the
     one-lane loop (pairing.h, BGV_MILLER=serial) produce the same Fp12 batch
     partial, byte for byte, and the same verdicts."""
     from lodestar_amd import native
