@@ -66,6 +66,7 @@ struct bgv_ctx {
   int msm_mode = -1;     // BGV_MSM=0|1 forces the signature combination (A/B tests); -1 = by batch shape
   bool overlap = true;    // BGV_OVERLAP=0 runs every stage on one stream (A/B tests)
   int split = -1;         // BGV_SPLIT=0|1 forces the latency mode (A/B tests); -1 = by batch size
+  int prefold = -1;       // BGV_PREFOLD=0|1 forces the two-level job fold (A/B tests); -1 = by batch shape
   int pairs = 0;          // BGV_PAIRS=1|2 forces sets per Miller work item (A/B tests); 0 = by batch size
   int sched = 0;          // BGV_SCHED bit mask of extra stream waits (A/B tests, run_stages)
   hipStream_t st = nullptr, st_hash = nullptr, st_pk = nullptr;
@@ -145,6 +146,7 @@ int bgv_open(int device, bgv_ctx** out) {
   if (const char* o = getenv("BGV_SCHED")) c->sched = atoi(o);
   if (const char* o = getenv("BGV_PAIRS")) c->pairs = atoi(o);
   if (const char* o = getenv("BGV_SPLIT")) c->split = atoi(o) != 0 ? 1 : 0;
+  if (const char* o = getenv("BGV_PREFOLD")) c->prefold = atoi(o) != 0 ? 1 : 0;
   // hash -> set-pair Miller is the critical path: its stream (and the pubkey
   // stream feeding it) get the highest priority, signature decode/scaling the
   // lowest (it only feeds the signature tree and the 1 pair per job)
@@ -354,6 +356,14 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, std::vector<uin
   d.split = c->split >= 0 ? (uint32_t)c->split : (n < 65536 ? 1u : 0u);
   // cooperative Miller loop (36 lanes per pair, low latency) unless the batch alone
   // fills the GPU, where the one-lane loop does less work per pair
+  // two-level per-job fold (bgv_tail.hip) when few jobs of >= 64 sets leave
+  // the chip idle: groups of ~sqrt(span) sets fold side by side, then the job
+  // folds the group values, 2 sqrt(span) sequential Fp12 products instead of span
+  {
+    const bool few_big = d.n_jobs <= 256 && d.span_log2 >= 6 && d.span_log2 <= 8;
+    const bool on = c->prefold >= 0 ? (c->prefold && d.span_log2 >= 2 && d.span_log2 <= 8) : few_big;
+    d.prefold_log2 = on ? (d.span_log2 + 1) / 2 : 0u;
+  }
   d.miller_coop = c->miller_mode >= 0 ? (uint32_t)c->miller_mode : (n < 65536 ? 1u : 0u);
   // sum r_i sigma_i per job by a bucket MSM (16 x 4-bit windows, ~1,800 G2
   // additions per 98-set job instead of 98 x 75 in per-set scalar mults)

@@ -57,9 +57,30 @@ __global__ void BGV_TREE_LB k_job_f(dev_batch b, dev_work w, uint32_t span) {
 // ------------------------------------------- cooperative folds (fp12_coop.h)
 #define COOP_LB __launch_bounds__(COOP_THREADS, 2)
 
+// first level of the two-level fold (few large jobs, e.g. one 64-set gossip
+// batch): workgroup (g, j) folds the job's sets [beg + G g, beg + G g + G)
+// into f_set[beg + G g] (in place: all reads precede the one write, and the
+// groups are disjoint); k_job_fold then walks the job with stride G
+__global__ void COOP_LB k_job_prefold(dev_batch b, dev_work w) {
+  __shared__ cscratch s;
+  __shared__ wfp12 acc, x;
+  const uint32_t j = blockIdx.y, G = 1u << b.prefold_log2;
+  const uint32_t beg = b.job_off[j], end = b.job_off[j + 1];
+  const uint32_t g0 = beg + blockIdx.x * G;
+  if (w.job_code[j] != C_OK || g0 + 1 >= end) return;  // uniform per workgroup
+  const uint32_t g1 = min(end, g0 + G);
+  c_load(&acc, w.f_set[g0]);
+  for (uint32_t i = g0 + 1; i < g1; i++) {
+    c_load(&x, w.f_set[i]);
+    c_mul(&acc, &acc, &x, &s);
+  }
+  c_store(w.f_set[g0], &acc);
+}
+
 // one workgroup per job: f_job = (job pair value) * prod of the job's set
-// values, folded in order at the latency of one Fp product per step
-__global__ void COOP_LB k_job_fold(dev_batch b, dev_work w) {
+// values (or of its group values after k_job_prefold, stride > 1), folded in
+// order at the latency of one Fp product per step
+__global__ void COOP_LB k_job_fold(dev_batch b, dev_work w, uint32_t stride) {
   __shared__ cscratch s;
   __shared__ wfp12 acc, x;
   const uint32_t j = blockIdx.x;
@@ -68,7 +89,7 @@ __global__ void COOP_LB k_job_fold(dev_batch b, dev_work w) {
     c_set_one(&acc);  // rejected jobs take no part in the batch product
   } else {
     c_load(&acc, w.f_set[b.n_sets + j]);
-    for (uint32_t i = beg; i < end; i++) {
+    for (uint32_t i = beg; i < end; i += stride) {
       c_load(&x, w.f_set[i]);
       c_mul(&acc, &acc, &x, &s);
     }
@@ -144,7 +165,12 @@ void launch_fp12_tail(hipStream_t st, int stage, const dev_batch& b, const dev_w
   if (stage == ST_F_TREE) {
     if (!b.n_jobs) return;
     if (span <= 256) {  // every job folds in one workgroup
-      hipLaunchKernelGGL(k_job_fold, dim3(b.n_jobs), ct, 0, st, b, w);
+      uint32_t stride = 1;
+      if (b.prefold_log2) {  // few large jobs: fold groups side by side first
+        stride = 1u << b.prefold_log2;
+        hipLaunchKernelGGL(k_job_prefold, dim3((span + stride - 1) / stride, b.n_jobs), ct, 0, st, b, w);
+      }
+      hipLaunchKernelGGL(k_job_fold, dim3(b.n_jobs), ct, 0, st, b, w, stride);
       return;
     }
     // larger jobs: segmented pairwise tree first

@@ -358,3 +358,37 @@ def test_latency_split_mode_bit_identical(monkeypatch):
     assert outs["0"][1:5] == outs["1"][1:5]
     assert outs["1"][2] == gexp and outs["1"][3] == gcodes
     assert outs["1"][4] == np.where(outs["1"][5], 0, 1).tolist()
+
+
+@pytest.mark.gpu
+def test_two_level_job_fold_bit_identical(monkeypatch):
+    """The two-level per-job fold (k_job_prefold, default for <= 256 jobs of
+    >= 64 sets: groups of ~sqrt(span) sets fold side by side, then the job
+    folds the group values) and the one-level fold (BGV_PREFOLD=0) give the
+    same batch partial, byte for byte, on ragged jobs (64, 100, 3, 1 and 132
+    sets), the same per-job verdicts when the batch check fails and every job
+    takes its own final exponentiation, and a passing batch when no set is
+    faulted."""
+    from lodestar_amd import native
+    offs = [0, 64, 164, 167, 168, 300]
+    outs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("BGV_PREFOLD", mode)
+        d = native.Device(0)
+        try:
+            d.gen_keys(1000, 256, 5)
+            res = []
+            for fault_every in (0, 150):  # 150: faults at sets 0 and 150 (jobs 0 and 1)
+                syn, bad = _synthetic_on(d, 300, 8, 1000, 256, 21, fault_every=fault_every)
+                syn["n_jobs"] = len(offs) - 1
+                syn["job_offsets"] = np.array(offs, np.uint32)
+                part, _, ok = d.partial(syn)
+                jr, _ = d.verify(syn)
+                want = [int(not bad[offs[j]:offs[j + 1]].any()) for j in range(len(offs) - 1)]
+                assert jr.tolist() == want
+                assert d.combine_final([part]) == (not bad.any())
+                res.append((part, ok, jr.tolist()))
+            outs[mode] = res
+        finally:
+            d.close()
+    assert outs["0"] == outs["1"]
