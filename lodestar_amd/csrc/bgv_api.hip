@@ -77,9 +77,16 @@ struct bgv_ctx {
   g1a* table = nullptr;
   uint32_t table_n = 0, table_cap = 0;
   dbuf<uint32_t> sk;
-  // staging for host batches
-  dbuf<uint32_t> job_off, pk_off, pk_idx, sig_len;
-  dbuf<uint8_t> raw_in, msgs, sigs, gen_out;
+  // staging for host batches: every host array of a batch is packed into one
+  // pinned buffer and crosses PCIe in ONE copy (pageable copies cost ~30-90 us
+  // each on the C2 critical path); results come back through pinned memory too
+  dbuf<uint8_t> stage_dev;
+  uint8_t* pin_in = nullptr;
+  uint8_t* pin_out = nullptr;
+  size_t pin_in_cap = 0, pin_out_cap = 0;
+  hipEvent_t ev_staged = nullptr;  // the last pin_in -> stage_dev copy
+  bool staged_pending = false;
+  dbuf<uint8_t> raw_in, gen_out;
   dbuf<uint64_t> scalars;
   dbuf<g1a> raw_conv;
   // per-batch intermediates
@@ -159,6 +166,7 @@ int bgv_open(int device, bgv_ctx** out) {
   for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
   for (auto& e : c->ev_end) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipEventCreate(&c->ev_fork));
+  HIPCHK(hipEventCreateWithFlags(&c->ev_staged, hipEventDisableTiming));
   *out = c;
   return BGV_OK;
 }
@@ -172,10 +180,13 @@ int bgv_close(bgv_ctx* c) {
   for (auto& e : c->ev) (void)hipEventDestroy(e);
   for (auto& e : c->ev_end) (void)hipEventDestroy(e);
   (void)hipEventDestroy(c->ev_fork);
+  (void)hipEventDestroy(c->ev_staged);
+  if (c->pin_in) (void)hipHostFree(c->pin_in);
+  if (c->pin_out) (void)hipHostFree(c->pin_out);
   if (c->table) (void)hipFree(c->table);
   c->sk.release();
-  c->job_off.release(); c->pk_off.release(); c->pk_idx.release(); c->sig_len.release();
-  c->raw_in.release(); c->msgs.release(); c->sigs.release(); c->gen_out.release();
+  c->stage_dev.release();
+  c->raw_in.release(); c->gen_out.release();
   c->scalars.release(); c->raw_conv.release();
   c->sig_aff.release(); c->h_aff.release(); c->sig_inf.release(); c->flags.release();
   c->sig_code.release(); c->pk_code.release(); c->job_code.release(); c->job_result.release(); c->set_code.release();
@@ -268,11 +279,47 @@ static void random_bytes(void* out, size_t n) {
   }
 }
 
-template <class T>
-static int stage_in(bgv_ctx* c, dbuf<T>& buf, const T* src, size_t n, const T*& dst) {
-  if (int r = buf.ensure(n ? n : 1)) return r;
-  if (n) HIPCHK(hipMemcpyAsync(buf.p, src, n * sizeof(T), hipMemcpyHostToDevice, c->st));
-  dst = buf.p;
+static int pinned_reserve(uint8_t*& p, size_t& cap, size_t n) {
+  if (n <= cap) return 0;
+  size_t c = cap ? cap : 65536;
+  while (c < n) c *= 2;
+  if (p) (void)hipHostFree(p);
+  p = nullptr;
+  cap = 0;
+  if (hipHostMalloc((void**)&p, c, hipHostMallocDefault) != hipSuccess) return fail(BGV_E_HIP, "hipHostMalloc(%zu) failed", c);
+  cap = c;
+  return 0;
+}
+
+// one host array of a batch, packed at a 256-byte aligned offset of the staging buffers
+struct stage_seg {
+  const void* src;
+  size_t bytes;
+  const void** dst;
+};
+
+// pack the segments into pin_in, copy them to stage_dev in one transfer and
+// point every *dst at its device copy
+static int stage_packed(bgv_ctx* c, stage_seg* segs, int n_segs) {
+  size_t total = 0;
+  for (int i = 0; i < n_segs; i++) total += (segs[i].bytes + 255) & ~size_t(255);
+  if (c->staged_pending) {  // the previous batch's copy may still read pin_in
+    HIPCHK(hipEventSynchronize(c->ev_staged));
+    c->staged_pending = false;
+  }
+  if (int r = pinned_reserve(c->pin_in, c->pin_in_cap, total ? total : 1)) return r;
+  if (int r = c->stage_dev.ensure(total ? total : 1)) return r;
+  size_t off = 0;
+  for (int i = 0; i < n_segs; i++) {
+    if (segs[i].bytes) memcpy(c->pin_in + off, segs[i].src, segs[i].bytes);
+    *segs[i].dst = c->stage_dev.p + off;
+    off += (segs[i].bytes + 255) & ~size_t(255);
+  }
+  if (total) {
+    HIPCHK(hipMemcpyAsync(c->stage_dev.p, c->pin_in, total, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipEventRecord(c->ev_staged, c->st));
+    c->staged_pending = true;
+  }
   return 0;
 }
 
@@ -314,16 +361,20 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, std::vector<uin
         return fail(BGV_E_TABLE_RANGE, "pubkey index %u >= table size %u", idx, c->table_n);
       }
     }
-    if (int r = stage_in(c, c->job_off, b->job_offsets, (size_t)J + 1, d.job_off)) return r;
-    if (int r = stage_in(c, c->pk_off, b->pk_offsets, (size_t)n + 1, d.pk_off)) return r;
-    if (int r = stage_in(c, c->pk_idx, b->pk_indices, (size_t)total, d.pk_idx)) return r;
-    if (int r = stage_in(c, c->msgs, b->msgs, (size_t)n * 32, d.msgs)) return r;
-    if (need_sigs) {
-      if (int r = stage_in(c, c->sigs, b->sigs, (size_t)n * 192, d.sigs)) return r;
-      if (int r = stage_in(c, c->sig_len, b->sig_len, (size_t)n, d.sig_len)) return r;
-    }
     const uint8_t* raw_dev = nullptr;
-    if (int r = stage_in(c, c->raw_in, b->raw_pks, (size_t)b->n_raw * 96, raw_dev)) return r;
+    stage_seg segs[8] = {
+        {b->job_offsets, ((size_t)J + 1) * 4, (const void**)&d.job_off},
+        {b->pk_offsets, ((size_t)n + 1) * 4, (const void**)&d.pk_off},
+        {b->pk_indices, (size_t)total * 4, (const void**)&d.pk_idx},
+        {b->msgs, (size_t)n * 32, (const void**)&d.msgs},
+        {b->raw_pks, (size_t)b->n_raw * 96, (const void**)&raw_dev},
+        {b->scalars, b->scalars ? (size_t)n * 8 : 0, (const void**)&d.scalars},
+        {b->sigs, need_sigs ? (size_t)n * 192 : 0, (const void**)&d.sigs},
+        {b->sig_len, need_sigs ? (size_t)n * 4 : 0, (const void**)&d.sig_len},
+    };
+    if (int r = stage_packed(c, segs, 8)) return r;
+    if (!b->scalars) d.scalars = nullptr;
+    if (!need_sigs) { d.sigs = nullptr; d.sig_len = nullptr; }
     if (int r = c->raw_conv.ensure(b->n_raw ? b->n_raw : 1)) return r;
     launch_raw_pks(c->st, raw_dev, c->raw_conv.p, b->n_raw);
     d.raw_pks = c->raw_conv.p;
@@ -371,7 +422,7 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, std::vector<uin
   // the per-set path, whose latency is one 64-bit scalar mult
   d.msm = c->msm_mode >= 0 ? (uint32_t)c->msm_mode : ((n >= 65536 && d.span_log2 <= 8) ? 1u : 0u);
   if (b->scalars && !b->on_device) {
-    if (int r = stage_in(c, c->scalars, b->scalars, (size_t)n, d.scalars)) return r;
+    // staged with the other host arrays above
   } else if (b->scalars) {
     d.scalars = b->scalars;
   } else {
@@ -478,11 +529,19 @@ int bgv_verify(bgv_ctx* c, const bgv_batch* b, int32_t* job_result, int32_t* set
   dev_work w;
   if (int r = work_alloc(c, d, w)) return r;
   if (int r = run_stages(c, d, w, 0, ST_COUNT)) return r;
-  if (d.n_jobs) HIPCHK(hipMemcpyAsync(job_result, w.job_result, (size_t)d.n_jobs * 4, hipMemcpyDeviceToHost, c->st));
-  if (set_code && d.n_sets) HIPCHK(hipMemcpyAsync(set_code, w.set_code, (size_t)d.n_sets * 4, hipMemcpyDeviceToHost, c->st));
-  uint32_t flag = 0;
-  HIPCHK(hipMemcpyAsync(&flag, w.flags, 4, hipMemcpyDeviceToHost, c->st));
+  // results through pinned memory: [flag | job_result | set_code]
+  const size_t jr_off = 256, sc_off = jr_off + (((size_t)d.n_jobs * 4 + 255) & ~size_t(255));
+  const bool want_sc = set_code && d.n_sets;
+  if (int r = pinned_reserve(c->pin_out, c->pin_out_cap, sc_off + (want_sc ? (size_t)d.n_sets * 4 : 0))) return r;
+  if (d.n_jobs) HIPCHK(hipMemcpyAsync(c->pin_out + jr_off, w.job_result, (size_t)d.n_jobs * 4, hipMemcpyDeviceToHost, c->st));
+  if (want_sc) HIPCHK(hipMemcpyAsync(c->pin_out + sc_off, w.set_code, (size_t)d.n_sets * 4, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipMemcpyAsync(c->pin_out, w.flags, 4, hipMemcpyDeviceToHost, c->st));
   HIPCHK(hipStreamSynchronize(c->st));
+  c->staged_pending = false;
+  uint32_t flag = 0;
+  memcpy(&flag, c->pin_out, 4);
+  if (d.n_jobs) memcpy(job_result, c->pin_out + jr_off, (size_t)d.n_jobs * 4);
+  if (want_sc) memcpy(set_code, c->pin_out + sc_off, (size_t)d.n_sets * 4);
   if (stats) {
     memset(stats, 0, sizeof *stats);
     for (int s = 0; s < ST_COUNT && s < BGV_N_STAGES; s++) HIPCHK(hipEventElapsedTime(&stats->stage_ms[s], c->ev[s], c->ev_end[s]));
