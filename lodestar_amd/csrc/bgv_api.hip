@@ -69,10 +69,14 @@ struct bgv_ctx {
   int prefold = -1;       // BGV_PREFOLD=0|1 forces the two-level job fold (A/B tests); -1 = by batch shape
   int pairs = 0;          // BGV_PAIRS=1|2 forces sets per Miller work item (A/B tests); 0 = by batch size
   int sched = 0;          // BGV_SCHED bit mask of extra stream waits (A/B tests, run_stages)
+  int timing = -1;        // BGV_TIMING=0|1: per-stage timing events; -1 = only for batches >= 65,536 sets
+  bool timed = true;      // the last run_stages recorded per-stage events
   hipStream_t st = nullptr, st_hash = nullptr, st_pk = nullptr;
   hipEvent_t ev[ST_COUNT + 1] = {};   // ev[s] = start of stage s on its stream
   hipEvent_t ev_end[ST_COUNT] = {};   // end of stage s on its stream
   hipEvent_t ev_fork = nullptr;
+  hipEvent_t ev_prep = nullptr;       // end of launch_prep (latency batches fork the hash leg before it)
+  hipEvent_t ev_dep[ST_COUNT] = {};   // untimed cross-stream dependencies (latency batches)
   // index2pubkey table (grown by copy) and synthetic secret keys
   g1a* table = nullptr;
   uint32_t table_n = 0, table_cap = 0;
@@ -154,6 +158,7 @@ int bgv_open(int device, bgv_ctx** out) {
   if (const char* o = getenv("BGV_PAIRS")) c->pairs = atoi(o);
   if (const char* o = getenv("BGV_SPLIT")) c->split = atoi(o) != 0 ? 1 : 0;
   if (const char* o = getenv("BGV_PREFOLD")) c->prefold = atoi(o) != 0 ? 1 : 0;
+  if (const char* o = getenv("BGV_TIMING")) c->timing = atoi(o) != 0 ? 1 : 0;
   // hash -> set-pair Miller is the critical path: its stream (and the pubkey
   // stream feeding it) get the highest priority, signature decode/scaling the
   // lowest (it only feeds the signature tree and the 1 pair per job)
@@ -167,6 +172,8 @@ int bgv_open(int device, bgv_ctx** out) {
   for (auto& e : c->ev_end) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipEventCreate(&c->ev_fork));
   HIPCHK(hipEventCreateWithFlags(&c->ev_staged, hipEventDisableTiming));
+  for (auto& e : c->ev_dep) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&c->ev_prep, hipEventDisableTiming));
   *out = c;
   return BGV_OK;
 }
@@ -181,6 +188,8 @@ int bgv_close(bgv_ctx* c) {
   for (auto& e : c->ev_end) (void)hipEventDestroy(e);
   (void)hipEventDestroy(c->ev_fork);
   (void)hipEventDestroy(c->ev_staged);
+  for (auto& e : c->ev_dep) (void)hipEventDestroy(e);
+  (void)hipEventDestroy(c->ev_prep);
   if (c->pin_in) (void)hipHostFree(c->pin_in);
   if (c->pin_out) (void)hipHostFree(c->pin_out);
   if (c->table) (void)hipFree(c->table);
@@ -482,40 +491,61 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
 // The set-pair Miller loops need only H(m) and the aggregated keys, so they
 // start while the signatures are still being scaled: at C4 the Miller kernel
 // fills 78% of the SIMDs (one wave each) and sig_scale takes the rest.
+// Per-stage timing events (stats->stage_ms) cost ~5 us of queue time each on
+// the critical path, so latency batches record only the stream dependencies
+// (untimed events) and the total.
 static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int from, int to) {
   const bool fork = c->overlap && from <= ST_SIG && to > ST_F_TREE;
+  const bool timed = c->timing >= 0 ? c->timing != 0 : d.n_sets >= 65536;
+  c->timed = timed;
+  hipEvent_t* dep = timed ? c->ev_end : c->ev_dep;  // what the stream waits below wait on
+  if (!timed) HIPCHK(hipEventRecord(c->ev[from], c->st));
+  // latency batches fork the hash leg BEFORE the index set-up: hash_to_G2 reads
+  // only the messages and heads the critical path (hash -> Miller -> fold ->
+  // final exp); large batches keep the set-up alone on the GPU (its
+  // one-workgroup scan starves under the bulk kernels)
+  const bool early_hash = fork && d.split && from <= ST_HASH && to > ST_HASH;
+  auto launch_one = [&](int s) -> int {
+    hipStream_t st = c->st;
+    if (fork) {
+      if (s == ST_HASH || s == ST_MILLER) st = c->st_hash;
+      if (s == ST_PK) st = c->st_pk;
+      if (s == ST_S_TREE || s == ST_MILLER) HIPCHK(hipStreamWaitEvent(st, dep[ST_PK], 0));
+      if (s == ST_F_TREE) HIPCHK(hipStreamWaitEvent(st, dep[ST_MILLER], 0));
+      // A/B knobs: hold the signature leg back so hash/pk (the Miller inputs) get the chip first
+      if (s == ST_SIG_SCALE && (c->sched & 1)) HIPCHK(hipStreamWaitEvent(st, dep[ST_HASH], 0));
+      if (s == ST_SIG && (c->sched & 2)) HIPCHK(hipStreamWaitEvent(st, dep[ST_HASH], 0));
+      if (s == ST_SIG_SCALE && (c->sched & 4)) HIPCHK(hipStreamWaitEvent(st, dep[ST_PK], 0));
+    }
+    if (timed) HIPCHK(hipEventRecord(c->ev[s], st));
+    launch_stage(st, s, d, w);
+    HIPCHK(hipGetLastError());
+    if (timed) HIPCHK(hipEventRecord(c->ev_end[s], st));
+    else if (fork && (s == ST_PK || s == ST_HASH || s == ST_MILLER)) HIPCHK(hipEventRecord(c->ev_dep[s], st));
+    return 0;
+  };
+  if (early_hash) {  // enqueued first, so the host's launch latency does not delay it either
+    HIPCHK(hipEventRecord(c->ev_fork, c->st));
+    HIPCHK(hipStreamWaitEvent(c->st_hash, c->ev_fork, 0));
+    if (int r = launch_one(ST_HASH)) return r;
+  }
   if (from <= ST_PK) {
     launch_prep(c->st, d, w);
     HIPCHK(hipGetLastError());
   }
   if (fork) {
-    HIPCHK(hipEventRecord(c->ev_fork, c->st));
-    HIPCHK(hipStreamWaitEvent(c->st_hash, c->ev_fork, 0));
-    HIPCHK(hipStreamWaitEvent(c->st_pk, c->ev_fork, 0));
+    HIPCHK(hipEventRecord(c->ev_prep, c->st));
+    if (!early_hash) HIPCHK(hipStreamWaitEvent(c->st_hash, c->ev_prep, 0));
+    HIPCHK(hipStreamWaitEvent(c->st_pk, c->ev_prep, 0));
   }
   int order[ST_COUNT], n_order = 0;
-  for (int s = from; s < to; s++) order[n_order++] = s;
-  if (fork && (c->sched & 2) && from == ST_SIG) {  // enqueue sig after hash/pk so it can wait on them
+  for (int s = from; s < to; s++)
+    if (!(early_hash && s == ST_HASH)) order[n_order++] = s;
+  if (fork && (c->sched & 2) && from == ST_SIG && !early_hash) {  // enqueue sig after hash/pk so it can wait on them
     order[0] = ST_HASH; order[1] = ST_PK; order[2] = ST_SIG;
   }
-  for (int oi = 0; oi < n_order; oi++) {
-    const int s = order[oi];
-    hipStream_t st = c->st;
-    if (fork) {
-      if (s == ST_HASH || s == ST_MILLER) st = c->st_hash;
-      if (s == ST_PK) st = c->st_pk;
-      if (s == ST_S_TREE || s == ST_MILLER) HIPCHK(hipStreamWaitEvent(st, c->ev_end[ST_PK], 0));
-      if (s == ST_F_TREE) HIPCHK(hipStreamWaitEvent(st, c->ev_end[ST_MILLER], 0));
-      // A/B knobs: hold the signature leg back so hash/pk (the Miller inputs) get the chip first
-      if (s == ST_SIG_SCALE && (c->sched & 1)) HIPCHK(hipStreamWaitEvent(st, c->ev_end[ST_HASH], 0));
-      if (s == ST_SIG && (c->sched & 2)) HIPCHK(hipStreamWaitEvent(st, c->ev_end[ST_HASH], 0));
-      if (s == ST_SIG_SCALE && (c->sched & 4)) HIPCHK(hipStreamWaitEvent(st, c->ev_end[ST_PK], 0));
-    }
-    HIPCHK(hipEventRecord(c->ev[s], st));
-    launch_stage(st, s, d, w);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev_end[s], st));
-  }
+  for (int oi = 0; oi < n_order; oi++)
+    if (int r = launch_one(order[oi])) return r;
   HIPCHK(hipEventRecord(c->ev[to], c->st));
   return 0;
 }
@@ -544,7 +574,8 @@ int bgv_verify(bgv_ctx* c, const bgv_batch* b, int32_t* job_result, int32_t* set
   if (want_sc) memcpy(set_code, c->pin_out + sc_off, (size_t)d.n_sets * 4);
   if (stats) {
     memset(stats, 0, sizeof *stats);
-    for (int s = 0; s < ST_COUNT && s < BGV_N_STAGES; s++) HIPCHK(hipEventElapsedTime(&stats->stage_ms[s], c->ev[s], c->ev_end[s]));
+    if (c->timed)
+      for (int s = 0; s < ST_COUNT && s < BGV_N_STAGES; s++) HIPCHK(hipEventElapsedTime(&stats->stage_ms[s], c->ev[s], c->ev_end[s]));
     HIPCHK(hipEventElapsedTime(&stats->total_ms, c->ev[0], c->ev[ST_COUNT]));
     stats->n_sets = d.n_sets;
     stats->n_jobs = d.n_jobs;
