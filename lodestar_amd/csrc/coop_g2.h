@@ -19,8 +19,13 @@ namespace bgv {
 constexpr int CG_LANES = 9;
 constexpr int CG_GROUPS = 64 / CG_LANES;  // 7 points per wave
 
+#ifndef BGV_CG_SPLIT_COMBINE
+#define BGV_CG_SPLIT_COMBINE 1
+#endif
+
 struct cg_scratch {
   fp_t P[3][3];  // [slot][sub-product]
+  fp_t O[3][2];  // [slot][c0, c1] (BGV_CG_SPLIT_COMBINE)
 };
 
 __device__ __forceinline__ fp2_t cg_sel(uint32_t s, const fp2_t& x0, const fp2_t& x1, const fp2_t& x2) {
@@ -54,9 +59,37 @@ __device__ void cg_round(cg_scratch* S, uint32_t s, uint32_t q, int n, const fp2
   fp_mul(r, u, v);
   if ((int)s < n) S->P[s][q] = r;
   coop_wave_sync();
+#if BGV_CG_SPLIT_COMBINE
+  // lane (s, 0) forms c0 = P0 - P1 of slot s, lane (s, 1) c1 = P2 - P0 - P1,
+  // then every lane reads the n products back: one more LDS exchange
+  // instead of 3 x 3 redundant additions on every lane
+  if ((int)s < n && q < 2) {
+    fp_t o;
+    if (q == 0) {
+      fp_sub(o, S->P[s][0], S->P[s][1]);
+    } else {
+      fp_t w;
+      fp_add(w, S->P[s][0], S->P[s][1]);
+      fp_sub(o, S->P[s][2], w);
+    }
+    S->O[s][q] = o;
+  }
+  coop_wave_sync();
+  o0.c0 = S->O[0][0];
+  o0.c1 = S->O[0][1];
+  if (n > 1) {
+    o1.c0 = S->O[1][0];
+    o1.c1 = S->O[1][1];
+  }
+  if (n > 2) {
+    o2.c0 = S->O[2][0];
+    o2.c1 = S->O[2][1];
+  }
+#else
   cg_combine(o0, S->P[0]);
   if (n > 1) cg_combine(o1, S->P[1]);
   if (n > 2) cg_combine(o2, S->P[2]);
+#endif
   coop_wave_sync();
 }
 
