@@ -23,6 +23,16 @@ constexpr int CG_GROUPS = 64 / CG_LANES;  // 7 points per wave
 #define BGV_CG_SPLIT_COMBINE 1
 #endif
 
+// force-inline the round and the point steps into the latency kernels (A/B knob)
+#ifndef BGV_CG_INLINE
+#define BGV_CG_INLINE 1  // k_hash_clear_coop 1.86 -> 1.77 ms, k_sig_split_coop 1.24 -> 1.17 ms (scratch 1936 -> 1504 B/lane)
+#endif
+#if BGV_CG_INLINE
+#define BGV_CGF __device__ __forceinline__
+#else
+#define BGV_CGF __device__
+#endif
+
 struct cg_scratch {
   fp_t P[3][3];  // [slot][sub-product]
   fp_t O[3][2];  // [slot][c0, c1] (BGV_CG_SPLIT_COMBINE)
@@ -40,7 +50,7 @@ __device__ __forceinline__ void cg_combine(fp2_t& o, const fp_t* P) {
 }
 
 // o_k = a_k * b_k for k < n (n <= 3); every lane of the group calls it
-__device__ void cg_round(cg_scratch* S, uint32_t s, uint32_t q, int n, const fp2_t& a0, const fp2_t& b0,
+BGV_CGF void cg_round(cg_scratch* S, uint32_t s, uint32_t q, int n, const fp2_t& a0, const fp2_t& b0,
                          const fp2_t& a1, const fp2_t& b1, const fp2_t& a2, const fp2_t& b2, fp2_t& o0, fp2_t& o1,
                          fp2_t& o2) {
   const fp2_t a = cg_sel(s, a0, a1, a2), b = cg_sel(s, b0, b1, b2);
@@ -94,7 +104,7 @@ __device__ void cg_round(cg_scratch* S, uint32_t s, uint32_t q, int n, const fp2
 }
 
 // dbl-2009-l (curve.h jac_dbl): 3 rounds
-__device__ void cg_dbl(cg_scratch* S, uint32_t s, uint32_t q, g2j& r, const g2j& p) {
+BGV_CGF void cg_dbl(cg_scratch* S, uint32_t s, uint32_t q, g2j& r, const g2j& p) {
   fp2_t A, B, T, C, Sq, F, E, t, D, x3, G, xb;
   cg_round(S, s, q, 3, p.x, p.x, p.y, p.y, p.y, p.z, A, B, T);
   fp2_dbl(E, A);
@@ -117,7 +127,7 @@ __device__ void cg_dbl(cg_scratch* S, uint32_t s, uint32_t q, g2j& r, const g2j&
 }
 
 // add-2007-bl with the exceptional cases (curve.h jac_add): 6 rounds
-__device__ void cg_add(cg_scratch* S, uint32_t s, uint32_t q, g2j& r, const g2j& p, const g2j& qq) {
+BGV_CGF void cg_add(cg_scratch* S, uint32_t s, uint32_t q, g2j& r, const g2j& p, const g2j& qq) {
   const bool pi = jac_is_inf(p), qi = jac_is_inf(qq);
   fp2_t z1z1, z2z2, zz, u1, u2, a, b, s1, s2, h, h2, i, j, v, rr, x, z3, x3, y, w, t, zs;
   fp2_add(zs, p.z, qq.z);
