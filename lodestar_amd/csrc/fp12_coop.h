@@ -27,6 +27,76 @@ struct cscratch {
 };
 
 // out = a * b (out may alias a or b)
+#ifndef BGV_COOP_LDS_AS
+#define BGV_COOP_LDS_AS 1
+#endif
+#if BGV_COOP_LDS_AS
+// c_mul is a non-inlined function whose operands all live in LDS; through the
+// generic pointers of its signature every access was a flat load/store
+// (waits on both the vector-memory and the LDS counters).  Casting them to
+// the LDS address space turns them into ds_read / ds_write.
+#define BGV_LDS __attribute__((address_space(3)))
+__device__ __forceinline__ fp_t lds_get(const BGV_LDS fp_t* p) {
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < NL; k++) r.l[k] = p->l[k];
+  return r;
+}
+__device__ __forceinline__ void lds_put(BGV_LDS fp_t* p, const fp_t& v) {
+#pragma unroll
+  for (int k = 0; k < NL; k++) p->l[k] = v.l[k];
+}
+
+__device__ void c_mul(wfp12* out_, const wfp12* a_, const wfp12* b_, cscratch* s_) {
+  BGV_LDS wfp12* out = (BGV_LDS wfp12*)out_;
+  const BGV_LDS wfp12* a = (const BGV_LDS wfp12*)a_;
+  const BGV_LDS wfp12* b = (const BGV_LDS wfp12*)b_;
+  BGV_LDS cscratch* s = (BGV_LDS cscratch*)s_;
+  const uint32_t l = threadIdx.x;
+  if (l < 108) {
+    const uint32_t p = l / 3, q = l - 3 * p, i = p / 6, j = p - 6 * i;
+    fp_t u, v;
+    if (q == 0) {
+      u = lds_get(&a->c[i].c0);
+      v = lds_get(&b->c[j].c0);
+    } else if (q == 1) {
+      u = lds_get(&a->c[i].c1);
+      v = lds_get(&b->c[j].c1);
+    } else {
+      fp_add_lazy(u, lds_get(&a->c[i].c0), lds_get(&a->c[i].c1));  // < 2p, product inputs only
+      fp_add_lazy(v, lds_get(&b->c[j].c0), lds_get(&b->c[j].c1));
+    }
+    fp_t r;
+    fp_mul(r, u, v);
+    lds_put(&s->p[l], r);
+  }
+  __syncthreads();
+  if (l < 36) {
+    const uint32_t i = l / 6, j = l - 6 * i;
+    const fp_t p0 = lds_get(&s->p[3 * l]), p1 = lds_get(&s->p[3 * l + 1]), p2 = lds_get(&s->p[3 * l + 2]);
+    fp2_t t;
+    fp_t w;
+    fp_sub(t.c0, p0, p1);
+    fp_add(w, p0, p1);
+    fp_sub(t.c1, p2, w);
+    if (i + j >= 6) fp2_mul_xi(t, t);
+    lds_put(&s->q[l].c0, t.c0);
+    lds_put(&s->q[l].c1, t.c1);
+  }
+  __syncthreads();
+  if (l < 12) {
+    const uint32_t k = l >> 1, comp = l & 1;
+    fp_t acc = lds_get(comp ? &s->q[k].c1 : &s->q[k].c0);  // i = 0, j = k
+#pragma unroll
+    for (uint32_t i = 1; i < 6; i++) {
+      const BGV_LDS fp2_t* t = &s->q[i * 6 + (k + 6 - i) % 6];
+      fp_add(acc, acc, lds_get(comp ? &t->c1 : &t->c0));
+    }
+    lds_put(comp ? &out->c[k].c1 : &out->c[k].c0, acc);
+  }
+  __syncthreads();
+}
+#else
 __device__ void c_mul(wfp12* out, const wfp12* a, const wfp12* b, cscratch* s) {
   const uint32_t l = threadIdx.x;
   if (l < 108) {
@@ -71,6 +141,7 @@ __device__ void c_mul(wfp12* out, const wfp12* a, const wfp12* b, cscratch* s) {
   }
   __syncthreads();
 }
+#endif
 
 __device__ void c_set_one(wfp12* r) {
   const uint32_t l = threadIdx.x;
