@@ -13,6 +13,7 @@
 // coordinates equal the one-lane kernels' (GPU test: latency mode on/off).
 #pragma once
 #include "miller_coop.h"
+#include "lds.h"
 
 namespace bgv {
 
@@ -67,35 +68,40 @@ BGV_CGF void cg_round(cg_scratch* S, uint32_t s, uint32_t q, int n, const fp2_t&
   }
   fp_t r;
   fp_mul(r, u, v);
-  if ((int)s < n) S->P[s][q] = r;
-  coop_wave_sync();
 #if BGV_CG_SPLIT_COMBINE
+  // S always points at the kernel's __shared__ scratch: LDS accesses (lds.h)
+  BGV_LDS cg_scratch* L = (BGV_LDS cg_scratch*)S;
+  if ((int)s < n) lds_put(&L->P[s][q], r);
+  coop_wave_sync();
   // lane (s, 0) forms c0 = P0 - P1 of slot s, lane (s, 1) c1 = P2 - P0 - P1,
   // then every lane reads the n products back: one more LDS exchange
   // instead of 3 x 3 redundant additions on every lane
   if ((int)s < n && q < 2) {
+    const fp_t p0 = lds_get(&L->P[s][0]), p1 = lds_get(&L->P[s][1]);
     fp_t o;
     if (q == 0) {
-      fp_sub(o, S->P[s][0], S->P[s][1]);
+      fp_sub(o, p0, p1);
     } else {
       fp_t w;
-      fp_add(w, S->P[s][0], S->P[s][1]);
-      fp_sub(o, S->P[s][2], w);
+      fp_add(w, p0, p1);
+      fp_sub(o, lds_get(&L->P[s][2]), w);
     }
-    S->O[s][q] = o;
+    lds_put(&L->O[s][q], o);
   }
   coop_wave_sync();
-  o0.c0 = S->O[0][0];
-  o0.c1 = S->O[0][1];
+  o0.c0 = lds_get(&L->O[0][0]);
+  o0.c1 = lds_get(&L->O[0][1]);
   if (n > 1) {
-    o1.c0 = S->O[1][0];
-    o1.c1 = S->O[1][1];
+    o1.c0 = lds_get(&L->O[1][0]);
+    o1.c1 = lds_get(&L->O[1][1]);
   }
   if (n > 2) {
-    o2.c0 = S->O[2][0];
-    o2.c1 = S->O[2][1];
+    o2.c0 = lds_get(&L->O[2][0]);
+    o2.c1 = lds_get(&L->O[2][1]);
   }
 #else
+  if ((int)s < n) S->P[s][q] = r;
+  coop_wave_sync();
   cg_combine(o0, S->P[0]);
   if (n > 1) cg_combine(o1, S->P[1]);
   if (n > 2) cg_combine(o2, S->P[2]);

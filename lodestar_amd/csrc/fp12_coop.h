@@ -15,6 +15,7 @@
 // Every function is called by all 128 threads (it contains __syncthreads()).
 #pragma once
 #include "fp12_wave.h"
+#include "lds.h"
 
 namespace bgv {
 
@@ -31,22 +32,8 @@ struct cscratch {
 #define BGV_COOP_LDS_AS 1
 #endif
 #if BGV_COOP_LDS_AS
-// c_mul is a non-inlined function whose operands all live in LDS; through the
-// generic pointers of its signature every access was a flat load/store
-// (waits on both the vector-memory and the LDS counters).  Casting them to
-// the LDS address space turns them into ds_read / ds_write.
-#define BGV_LDS __attribute__((address_space(3)))
-__device__ __forceinline__ fp_t lds_get(const BGV_LDS fp_t* p) {
-  fp_t r;
-#pragma unroll
-  for (int k = 0; k < NL; k++) r.l[k] = p->l[k];
-  return r;
-}
-__device__ __forceinline__ void lds_put(BGV_LDS fp_t* p, const fp_t& v) {
-#pragma unroll
-  for (int k = 0; k < NL; k++) p->l[k] = v.l[k];
-}
-
+// c_mul is a non-inlined function whose operands all live in LDS: the
+// casts below make its accesses ds_read / ds_write (lds.h)
 __device__ void c_mul(wfp12* out_, const wfp12* a_, const wfp12* b_, cscratch* s_) {
   BGV_LDS wfp12* out = (BGV_LDS wfp12*)out_;
   const BGV_LDS wfp12* a = (const BGV_LDS wfp12*)a_;
