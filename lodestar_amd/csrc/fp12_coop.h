@@ -217,14 +217,19 @@ __device__ void c_frob(wfp12* out, const wfp12* a, int k, cscratch* s) {
 //            squaring ((u0 + u1)(u0 - u1) | u0 u1)
 //   round 2  lane l < 12: component l % 2 of output coefficient l / 2
 // out may alias a (each round-2 lane reads and writes only its component).
-__device__ void c_cyc_sqr(wfp12* out, const wfp12* a, cscratch* s) {
+__device__ void c_cyc_sqr(wfp12* out_, const wfp12* a_, cscratch* s_) {
+  // every operand lives in LDS (lds.h)
+  BGV_LDS wfp12* out = (BGV_LDS wfp12*)out_;
+  const BGV_LDS wfp12* a = (const BGV_LDS wfp12*)a_;
+  BGV_LDS cscratch* s = (BGV_LDS cscratch*)s_;
+  auto get2 = [](const BGV_LDS fp2_t* p) { fp2_t r; r.c0 = lds_get(&p->c0); r.c1 = lds_get(&p->c1); return r; };
   const uint32_t l = threadIdx.x;
   if (l < 18) {
     const uint32_t f = l / 6, r = l - 6 * f, k = r >> 1, comp = r & 1;
     fp2_t x;
-    if (k == 0) x = a->c[f];
-    else if (k == 1) x = a->c[f + 3];
-    else fp2_add(x, a->c[f], a->c[f + 3]);
+    if (k == 0) x = get2(&a->c[f]);
+    else if (k == 1) x = get2(&a->c[f + 3]);
+    else fp2_add(x, get2(&a->c[f]), get2(&a->c[f + 3]));
     fp_t u, v;
     if (comp == 0) {
       fp_add_lazy(u, x.c0, x.c1);  // < 2p, product input only
@@ -233,7 +238,9 @@ __device__ void c_cyc_sqr(wfp12* out, const wfp12* a, cscratch* s) {
       u = x.c0;
       v = x.c1;
     }
-    fp_mul(s->p[l], u, v);
+    fp_t pr;
+    fp_mul(pr, u, v);
+    lds_put(&s->p[l], pr);
   }
   __syncthreads();
   if (l < 12) {
@@ -243,8 +250,8 @@ __device__ void c_cyc_sqr(wfp12* out, const wfp12* a, cscratch* s) {
     fp2_t S[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-      S[k].c0 = s->p[6 * f + 2 * k];
-      fp_dbl(S[k].c1, s->p[6 * f + 2 * k + 1]);
+      S[k].c0 = lds_get(&s->p[6 * f + 2 * k]);
+      fp_dbl(S[k].c1, lds_get(&s->p[6 * f + 2 * k + 1]));
     }
     fp2_t T0, T1, t;
     fp2_mul_xi(t, S[1]);
@@ -256,15 +263,14 @@ __device__ void c_cyc_sqr(wfp12* out, const wfp12* a, cscratch* s) {
     else if (j == 1) fp2_mul_xi(V, T1);
     else V = T1;
     const fp_t& v = comp ? V.c1 : V.c0;
-    const fp_t& g = comp ? a->c[j].c1 : a->c[j].c0;
+    const fp_t g = lds_get(comp ? &a->c[j].c1 : &a->c[j].c0);
     fp_t v3, g2, r;
     fp_add(v3, v, v);
     fp_add(v3, v3, v);
     fp_dbl(g2, g);
     if (j & 1) fp_add(r, v3, g2);
     else fp_sub(r, v3, g2);
-    if (comp) out->c[j].c1 = r;
-    else out->c[j].c0 = r;
+    lds_put(comp ? &out->c[j].c1 : &out->c[j].c0, r);
   }
   __syncthreads();
 }
