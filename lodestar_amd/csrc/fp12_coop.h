@@ -276,7 +276,7 @@ __device__ void c_cyc_sqr(wfp12* out_, const wfp12* a_, cscratch* s_) {
 }
 
 #ifndef BGV_COOP_CYC_SQR
-#define BGV_COOP_CYC_SQR 0  // measured: batch final exp 2.10 ms against 1.98 with c_mul (latency is the lone wave's product chain, not the rounds)
+#define BGV_COOP_CYC_SQR 0  // measured: batch final exp 2.10 ms against 1.98 with c_mul; both through LDS address-space pointers, 2.07 against 1.68
 #endif
 
 // out = a^x (x < 0) for a in the cyclotomic subgroup
