@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define BGV_ABI_VERSION 1
+#define BGV_ABI_VERSION 2
 
 /* ---- status of an API call (negative) ---------------------------------- */
 enum bgv_status {
@@ -35,6 +35,9 @@ enum bgv_status {
   BGV_E_NO_DEVICE = -3,
   BGV_E_TABLE_RANGE = -4,  /* pubkey index outside the resident table */
   BGV_E_EMPTY_SET = -5,    /* a set with zero pubkeys (EMPTY_AGGREGATE_ARRAY) */
+  BGV_E_BAD_PUBKEY = -6,   /* bgv_pubkeys_set: a key does not deserialize (the
+                              text names the key and its BLST_* code) */
+  BGV_E_STATE = -7,        /* bgv_partial_finish without a preceding bgv_partial */
 };
 
 /* ---- per-set / per-job outcome codes (>= 0) ------------------------------
@@ -84,6 +87,17 @@ typedef struct bgv_ctx bgv_ctx;
  * pk_offsets[i+1]).  An index with bit 31 set selects entry
  * (index & 0x7fffffff) of raw_pks instead (pubkeys not in the table, e.g.
  * BLS-to-execution changes, signatureSets/blsToExecutionChange.ts:32).
+ * An index past the table (or past n_raw) rejects only its job, with set
+ * code BGV_SET_INDEX_RANGE: the reference fails such a lookup on the caller's
+ * side (index2pubkey[i] is undefined), so other co-batched jobs are unaffected.
+ * A set with no pubkeys fails the whole call with BGV_E_EMPTY_SET (callers
+ * reject EMPTY_AGGREGATE_ARRAY before batching, chain/bls/utils.ts:11).
+ * Host batches are copied into pinned staging memory first and every
+ * contract check runs on that copy, so a caller that mutates its arrays
+ * during the call cannot make the device read out of bounds.  On-device
+ * batches (on_device = 1) are trusted to satisfy the contract: offsets
+ * monotone, job_offsets spanning [0, n_sets], pk_indices as long as
+ * pk_offsets[n_sets].
  *
  * Signatures: sig_len[i] bytes at sigs + 192*i (96 = compressed,
  * 192 = uncompressed; any other length yields BGV_SET_INVALID_SIZE, the
@@ -116,7 +130,7 @@ typedef struct bgv_batch {
  * the stream it ran on; stages 0-3 run concurrently on three streams, so their
  * times overlap and total_ms is less than their sum) plus the counters the reference pool exports as
  * lodestar_bls_thread_pool_* metrics (metrics/metrics/lodestar.ts:350-430). */
-#define BGV_N_STAGES 12
+#define BGV_N_STAGES 16
 typedef struct bgv_stats {
   float stage_ms[BGV_N_STAGES]; /* see bgv_stage_name() */
   float total_ms;
@@ -142,7 +156,15 @@ int bgv_close(bgv_ctx* ctx);
 /* index2pubkey table management: mirrors syncPubkeys / addPubkey
  * (state-transition/src/cache/pubkeyCache.ts:56-77, cache/epochContext.ts:
  * 701-704).  Keys are trusted (validated at deposit, block/processDeposit.ts:
- * 57-66) and stored as affine Montgomery (x, y), 96 B per validator.     */
+ * 57-66) and stored as affine Montgomery (x, y), 96 B per validator.
+ * Like PublicKey.fromBytes(pk, jacobian) (no validation) a key must still
+ * deserialize: flags, x < p, on the curve; otherwise the call fails with
+ * BGV_E_BAD_PUBKEY and the table is unchanged.  The infinity key is stored
+ * as the identity (a set aggregating only identities is BLST_PK_IS_INFINITY).
+ * The table is append-only like syncPubkeys: first_index <= current count
+ * (rows below the count may be rewritten, as addPubkey does); a gap fails
+ * with BGV_E_TABLE_RANGE.  At most 2^31 - 1 rows (bit 31 of an index
+ * selects raw_pks).                                                       */
 int bgv_pubkeys_set(bgv_ctx* ctx, uint32_t first_index, uint32_t n, const uint8_t* data, uint32_t format);
 int bgv_pubkeys_count(bgv_ctx* ctx, uint32_t* count);
 /* read back entries as 96-byte uncompressed big-endian (tests, checkpoints) */
@@ -167,15 +189,53 @@ int bgv_pubkeys_validate(bgv_ctx* ctx, const uint8_t* pk48, uint32_t n, int32_t*
  * One whole-batch pairing check runs first; only when it fails is every
  * job checked on its own (the worker's per-job retry, worker.ts:74-85). */
 int bgv_verify(bgv_ctx* ctx, const bgv_batch* batch, int32_t* job_result, int32_t* set_code, bgv_stats* stats);
+/* Stage timings (stage_ms, total_ms) of the last pipeline run on the context
+ * (bgv_verify, bgv_partial, bgv_partial_finish); counters are left zero. */
+int bgv_last_stats(bgv_ctx* ctx, bgv_stats* stats);
 
 /* Multi-GPU partials: run the batch up to, but excluding, the
  * final exponentiation and return this shard's Miller product (576 B, 12
  * Fp coefficients of w^0..w^5, c0||c1 each, 48-byte big-endian) with the
- * per-set codes.  ok_out = 1 when no set failed to parse. */
-int bgv_partial(bgv_ctx* ctx, const bgv_batch* batch, uint8_t* miller576, int32_t* set_code, int32_t* ok_out);
+ * per-set codes and per-job provisional results (job_result may be NULL):
+ * -code for a job rejected by a parse / subgroup / pubkey error (final),
+ * 1 for every other job (valid iff the node's combined check passes).
+ * ok_out = 1 when no job was rejected.  The shard's intermediates stay on
+ * the context for bgv_partial_finish until the next call on it. */
+int bgv_partial(bgv_ctx* ctx, const bgv_batch* batch, uint8_t* miller576, int32_t* set_code, int32_t* job_result,
+                int32_t* ok_out);
+/* Localisation after a failed combined check (SURVEY §8e "Failure"): the
+ * final exponentiation of THIS shard's product, then per-job final
+ * exponentiations only if it fails (the worker's per-job retry,
+ * multithread/worker.ts:74-85), on the intermediates bgv_partial left.
+ * job_result[n_jobs] as for bgv_verify.  BGV_E_STATE when the previous call
+ * on the context was not bgv_partial. */
+int bgv_partial_finish(bgv_ctx* ctx, int32_t* job_result, bgv_stats* stats);
 /* Combine n partial Miller products and run ONE final exponentiation:
  * *is_one = 1 iff the product maps to 1 in GT. */
 int bgv_combine_final(bgv_ctx* ctx, const uint8_t* millers576, uint32_t n, int32_t* is_one);
+
+/* ---- test-only: per-stage intermediates (SURVEY §8c golden plan) --------
+ * Runs bgv_verify on the batch and copies out the canonical values of every
+ * stage.  Points are affine, plain big-endian: G1 x || y (96 B), G2
+ * x.c0 || x.c1 || y.c0 || y.c1 (192 B); the identity and rejected entries
+ * are all-zero.  GT values are 576 B as for bgv_partial and are the cube of
+ * the textbook final exponentiation f^((p^12 - 1)/r) (the hard-part chain
+ * computes 3 (p^4 - p^2 + 1)/r).  Any pointer may be NULL.
+ *   pair_fe[n_sets + n_jobs]: FE of every Miller value: set pairs first
+ *   (with two pairs per Miller work item, n_sets >= 65,536 or BGV_PAIRS=2,
+ *   entry 2k holds the item's product and 2k+1 the identity), then each
+ *   job's (-G1, S_job) pair. */
+typedef struct bgv_debug {
+  uint8_t* sig_aff;  /* [n_sets][192] decoded signature (zero: invalid / identity) */
+  uint8_t* h_aff;    /* [n_sets][192] H(m_i) */
+  uint8_t* pk_agg;   /* [n_sets][96]  aggregated pubkey before the batch scalar */
+  uint8_t* rpk_aff;  /* [n_sets][96]  r_i * aggregated pubkey */
+  uint8_t* s_aff;    /* [n_jobs][192] S_job = sum over the job of r_i sigma_i */
+  uint8_t* pair_fe;  /* [n_sets + n_jobs][576] */
+  uint8_t* job_fe;   /* [n_jobs][576] FE of the job's Miller product */
+  uint8_t* batch_fe; /* [576] FE of the whole-batch product */
+} bgv_debug;
+int bgv_debug_stages(bgv_ctx* ctx, const bgv_batch* batch, int32_t* job_result, int32_t* set_code, bgv_debug* out);
 
 /* ---- synthetic workload generation (bench / tests; not on the verify path) */
 /* table[first .. first+n) := sk_i * G1 with sk_i = SHA256("bgv-sk" || LE64(seed)

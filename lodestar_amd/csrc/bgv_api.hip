@@ -68,9 +68,9 @@ struct bgv_ctx {
   int split = -1;         // BGV_SPLIT=0|1 forces the latency mode (A/B tests); -1 = by batch size
   int prefold = -1;       // BGV_PREFOLD=0|1 forces the two-level job fold (A/B tests); -1 = by batch shape
   int pairs = 0;          // BGV_PAIRS=1|2 forces sets per Miller work item (A/B tests); 0 = by batch size
-  int sched = 0;          // BGV_SCHED bit mask of extra stream waits (A/B tests, run_stages)
   int timing = -1;        // BGV_TIMING=0|1: per-stage timing events; -1 = only for batches >= 65,536 sets
   bool timed = true;      // the last run_stages recorded per-stage events
+  int run_from = 0, run_to = 0;  // stage range of the last run_stages (bgv_last_stats)
   hipStream_t st = nullptr, st_hash = nullptr, st_pk = nullptr;
   hipEvent_t ev[ST_COUNT + 1] = {};   // ev[s] = start of stage s on its stream
   hipEvent_t ev_end[ST_COUNT] = {};   // end of stage s on its stream
@@ -91,6 +91,20 @@ struct bgv_ctx {
   hipEvent_t ev_staged = nullptr;  // the last pin_in -> stage_dev copy
   bool staged_pending = false;
   dbuf<uint8_t> raw_in, gen_out;
+  dbuf<g1a> pk_tmp;         // bgv_pubkeys_set: decoded rows before they enter the table
+  dbuf<int32_t> pk_codes;   // bgv_pubkeys_set: per-key deserialization codes
+  std::vector<int32_t> pk_codes_host;
+  // host view of the last prepared batch (offsets from the pinned copy or HBM)
+  std::vector<uint32_t> jo_host;
+  uint32_t pk_total = 0;
+  // bgv_partial -> bgv_partial_finish: the shard's intermediates stay resident
+  bool partial_pending = false;
+  dev_batch part_d;
+  dev_work part_w;
+  // bgv_debug_stages
+  dbuf<g1a> pk_agg;
+  dbuf<fp12_t> dbg_fe;
+  dbuf<uint8_t> dbg_out;
   dbuf<uint64_t> scalars;
   dbuf<g1a> raw_conv;
   // per-batch intermediates
@@ -135,10 +149,11 @@ const char* bgv_set_code_name(int code) {
 }
 
 const char* bgv_stage_name(int stage) {
-  static const char* names[ST_COUNT] = {"sig_decode_subgroup", "hash_to_g2",          "pk_aggregate_scale",
-                                        "sig_scale",           "sig_sum_tree",        "miller_loop",
-                                        "miller_loop_jobs",    "miller_product_tree", "batch_product",
-                                        "batch_final_exp",     "job_final_exp",       "set_codes"};
+  static const char* names[ST_COUNT] = {"sig_decode_subgroup", "hash_to_g2",       "pk_gather",
+                                        "pk_aggregate_scale",  "sig_scale",        "sig_sum_tree",
+                                        "miller_loop",         "miller_loop_jobs", "miller_product_tree",
+                                        "batch_product",       "batch_final_exp",  "job_final_exp",
+                                        "set_codes"};
   return (stage >= 0 && stage < ST_COUNT) ? names[stage] : "unknown";
 }
 
@@ -154,7 +169,6 @@ int bgv_open(int device, bgv_ctx** out) {
   if (const char* m = getenv("BGV_MILLER")) c->miller_mode = strcmp(m, "serial") != 0 ? 1 : 0;
   if (const char* m = getenv("BGV_MSM")) c->msm_mode = strcmp(m, "0") != 0 ? 1 : 0;
   if (const char* o = getenv("BGV_OVERLAP")) c->overlap = strcmp(o, "0") != 0;
-  if (const char* o = getenv("BGV_SCHED")) c->sched = atoi(o);
   if (const char* o = getenv("BGV_PAIRS")) c->pairs = atoi(o);
   if (const char* o = getenv("BGV_SPLIT")) c->split = atoi(o) != 0 ? 1 : 0;
   if (const char* o = getenv("BGV_PREFOLD")) c->prefold = atoi(o) != 0 ? 1 : 0;
@@ -195,7 +209,8 @@ int bgv_close(bgv_ctx* c) {
   if (c->table) (void)hipFree(c->table);
   c->sk.release();
   c->stage_dev.release();
-  c->raw_in.release(); c->gen_out.release();
+  c->raw_in.release(); c->gen_out.release(); c->pk_tmp.release(); c->pk_codes.release();
+  c->pk_agg.release(); c->dbg_fe.release(); c->dbg_out.release();
   c->scalars.release(); c->raw_conv.release();
   c->sig_aff.release(); c->h_aff.release(); c->sig_inf.release(); c->flags.release();
   c->sig_code.release(); c->pk_code.release(); c->job_code.release(); c->job_result.release(); c->set_code.release();
@@ -227,18 +242,34 @@ static int table_reserve(bgv_ctx* c, uint32_t n) {
   return 0;
 }
 
+// index2pubkey rows are u32 indices with bit 31 reserved for raw_pks
+static const uint32_t TABLE_MAX = 0x7fffffffu;
+
 int bgv_pubkeys_set(bgv_ctx* c, uint32_t first, uint32_t n, const uint8_t* data, uint32_t fmt) {
   if (!c || (!data && n)) return fail(BGV_E_INVALID_ARG, "null argument");
   if (fmt != BGV_PK_COMPRESSED_48 && fmt != BGV_PK_UNCOMPRESSED_96) return fail(BGV_E_INVALID_ARG, "bad format %u", fmt);
+  c->partial_pending = false;
   if (n == 0) return BGV_OK;
+  if ((uint64_t)first + n > TABLE_MAX) return fail(BGV_E_TABLE_RANGE, "rows [%u, %llu) exceed the table limit 2^31 - 1", first, (unsigned long long)first + n);
+  if (first > c->table_n)
+    return fail(BGV_E_TABLE_RANGE, "row %u would leave a gap after the %u rows of the table (append-only, pubkeyCache.ts:56-77)", first, c->table_n);
   HIPCHK(hipSetDevice(c->device));
   if (int r = table_reserve(c, first + n)) return r;
   const size_t w = fmt == BGV_PK_COMPRESSED_48 ? 48 : 96;
   if (int r = c->raw_in.ensure((size_t)n * w)) return r;
+  if (int r = c->pk_tmp.ensure(n)) return r;
+  if (int r = c->pk_codes.ensure(n)) return r;
   HIPCHK(hipMemcpyAsync(c->raw_in.p, data, (size_t)n * w, hipMemcpyHostToDevice, c->st));
-  if (fmt == BGV_PK_COMPRESSED_48) launch_table_from_compressed(c->st, c->raw_in.p, c->table + first, n);
-  else launch_table_from_uncompressed(c->st, c->raw_in.p, c->table + first, n);
+  if (fmt == BGV_PK_COMPRESSED_48) launch_table_from_compressed(c->st, c->raw_in.p, c->pk_tmp.p, n, c->pk_codes.p);
+  else launch_table_from_uncompressed(c->st, c->raw_in.p, c->pk_tmp.p, n, c->pk_codes.p);
   HIPCHK(hipGetLastError());
+  c->pk_codes_host.resize(n);
+  HIPCHK(hipMemcpyAsync(c->pk_codes_host.data(), c->pk_codes.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  for (uint32_t i = 0; i < n; i++)
+    if (c->pk_codes_host[i] != 0)  // PublicKey.fromBytes throws: nothing is stored
+      return fail(BGV_E_BAD_PUBKEY, "pubkey %u: BLST_ERROR: %s", first + i, bgv_set_code_name(c->pk_codes_host[i]));
+  HIPCHK(hipMemcpyAsync(c->table + first, c->pk_tmp.p, (size_t)n * sizeof(g1a), hipMemcpyDeviceToDevice, c->st));
   HIPCHK(hipStreamSynchronize(c->st));
   if (first + n > c->table_n) c->table_n = first + n;
   return BGV_OK;
@@ -305,12 +336,13 @@ struct stage_seg {
   const void* src;
   size_t bytes;
   const void** dst;
+  size_t off;  // filled by stage_pack: offset in pin_in / stage_dev
 };
 
-// pack the segments into pin_in, copy them to stage_dev in one transfer and
-// point every *dst at its device copy
-static int stage_packed(bgv_ctx* c, stage_seg* segs, int n_segs) {
-  size_t total = 0;
+// pack the segments into pin_in (host copies only) and point every *dst at
+// its future device copy; stage_issue then moves the whole buffer in one transfer
+static int stage_pack(bgv_ctx* c, stage_seg* segs, int n_segs, size_t& total) {
+  total = 0;
   for (int i = 0; i < n_segs; i++) total += (segs[i].bytes + 255) & ~size_t(255);
   if (c->staged_pending) {  // the previous batch's copy may still read pin_in
     HIPCHK(hipEventSynchronize(c->ev_staged));
@@ -321,19 +353,27 @@ static int stage_packed(bgv_ctx* c, stage_seg* segs, int n_segs) {
   size_t off = 0;
   for (int i = 0; i < n_segs; i++) {
     if (segs[i].bytes) memcpy(c->pin_in + off, segs[i].src, segs[i].bytes);
+    segs[i].off = off;
     *segs[i].dst = c->stage_dev.p + off;
     off += (segs[i].bytes + 255) & ~size_t(255);
-  }
-  if (total) {
-    HIPCHK(hipMemcpyAsync(c->stage_dev.p, c->pin_in, total, hipMemcpyHostToDevice, c->st));
-    HIPCHK(hipEventRecord(c->ev_staged, c->st));
-    c->staged_pending = true;
   }
   return 0;
 }
 
+static int stage_issue(bgv_ctx* c, size_t total) {
+  if (!total) return 0;
+  HIPCHK(hipMemcpyAsync(c->stage_dev.p, c->pin_in, total, hipMemcpyHostToDevice, c->st));
+  HIPCHK(hipEventRecord(c->ev_staged, c->st));
+  c->staged_pending = true;
+  return 0;
+}
+
 // Build the device view of a batch: stage host arrays, convert raw pubkeys.
-static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, std::vector<uint64_t>& scal_host, bool need_sigs) {
+// Host batches: the arrays are copied into pinned memory FIRST and every
+// contract check reads that copy, so the device only ever sees checked
+// offsets even if the caller's buffers change during the call.  Index ranges
+// are checked per set on the device (BGV_SET_INDEX_RANGE rejects the job).
+static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs) {
   if (!b) return fail(BGV_E_INVALID_ARG, "batch is NULL");
   if (!b->job_offsets || !b->pk_offsets || !b->pk_indices || !b->msgs || (need_sigs && (!b->sigs || !b->sig_len)))
     return fail(BGV_E_INVALID_ARG, "missing batch array");
@@ -346,42 +386,42 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, std::vector<uin
   d.table_n = c->table_n;
   d.table = c->table;
   d.span_log2 = 7;  // device batches: trees cover jobs of <= 128 sets (multithread/index.ts:39)
+  c->jo_host.resize((size_t)J + 1);
   if (!b->on_device) {
-    // host-side contract checks (the reference rejects these synchronously)
-    if (b->job_offsets[0] != 0 || b->job_offsets[J] != n) return fail(BGV_E_INVALID_ARG, "job_offsets must span [0, n_sets]");
+    const uint32_t total = b->pk_offsets[n];  // sizes the pk_indices copy; re-checked on the copy
+    const uint8_t* raw_dev = nullptr;
+    stage_seg segs[8] = {
+        {b->job_offsets, ((size_t)J + 1) * 4, (const void**)&d.job_off, 0},
+        {b->pk_offsets, ((size_t)n + 1) * 4, (const void**)&d.pk_off, 0},
+        {b->pk_indices, (size_t)total * 4, (const void**)&d.pk_idx, 0},
+        {b->msgs, (size_t)n * 32, (const void**)&d.msgs, 0},
+        {b->raw_pks, (size_t)b->n_raw * 96, (const void**)&raw_dev, 0},
+        {b->scalars, b->scalars ? (size_t)n * 8 : 0, (const void**)&d.scalars, 0},
+        {b->sigs, need_sigs ? (size_t)n * 192 : 0, (const void**)&d.sigs, 0},
+        {b->sig_len, need_sigs ? (size_t)n * 4 : 0, (const void**)&d.sig_len, 0},
+    };
+    size_t bytes = 0;
+    if (int r = stage_pack(c, segs, 8, bytes)) return r;
+    const uint32_t* jo = (const uint32_t*)(c->pin_in + segs[0].off);
+    const uint32_t* po = (const uint32_t*)(c->pin_in + segs[1].off);
+    // host-side contract checks on the pinned copy (the reference rejects these synchronously)
+    if (jo[0] != 0 || jo[J] != n) return fail(BGV_E_INVALID_ARG, "job_offsets must span [0, n_sets]");
     uint32_t max_job = 1;
     for (uint32_t j = 0; j < J; j++) {
-      if (b->job_offsets[j + 1] < b->job_offsets[j]) return fail(BGV_E_INVALID_ARG, "job_offsets not monotone");
-      if (b->job_offsets[j + 1] - b->job_offsets[j] > max_job) max_job = b->job_offsets[j + 1] - b->job_offsets[j];
+      if (jo[j + 1] < jo[j]) return fail(BGV_E_INVALID_ARG, "job_offsets not monotone");
+      if (jo[j + 1] - jo[j] > max_job) max_job = jo[j + 1] - jo[j];
     }
     d.span_log2 = 0;
     while ((1u << d.span_log2) < max_job && d.span_log2 < 16) d.span_log2++;
-    if (b->pk_offsets[0] != 0) return fail(BGV_E_INVALID_ARG, "pk_offsets[0] != 0");
+    if (po[0] != 0) return fail(BGV_E_INVALID_ARG, "pk_offsets[0] != 0");
+    if (po[n] != total) return fail(BGV_E_INVALID_ARG, "pk_offsets changed during the call");
     for (uint32_t i = 0; i < n; i++) {
-      if (b->pk_offsets[i + 1] < b->pk_offsets[i]) return fail(BGV_E_INVALID_ARG, "pk_offsets not monotone");
-      if (b->pk_offsets[i + 1] == b->pk_offsets[i]) return fail(BGV_E_EMPTY_SET, "EMPTY_AGGREGATE_ARRAY (set %u)", i);
+      if (po[i + 1] < po[i]) return fail(BGV_E_INVALID_ARG, "pk_offsets not monotone");
+      if (po[i + 1] == po[i]) return fail(BGV_E_EMPTY_SET, "EMPTY_AGGREGATE_ARRAY (set %u)", i);
     }
-    const uint32_t total = b->pk_offsets[n];
-    for (uint32_t k = 0; k < total; k++) {
-      const uint32_t idx = b->pk_indices[k];
-      if (idx & 0x80000000u) {
-        if ((idx & 0x7fffffffu) >= b->n_raw) return fail(BGV_E_TABLE_RANGE, "raw pubkey index %u >= n_raw %u", idx & 0x7fffffffu, b->n_raw);
-      } else if (idx >= c->table_n) {
-        return fail(BGV_E_TABLE_RANGE, "pubkey index %u >= table size %u", idx, c->table_n);
-      }
-    }
-    const uint8_t* raw_dev = nullptr;
-    stage_seg segs[8] = {
-        {b->job_offsets, ((size_t)J + 1) * 4, (const void**)&d.job_off},
-        {b->pk_offsets, ((size_t)n + 1) * 4, (const void**)&d.pk_off},
-        {b->pk_indices, (size_t)total * 4, (const void**)&d.pk_idx},
-        {b->msgs, (size_t)n * 32, (const void**)&d.msgs},
-        {b->raw_pks, (size_t)b->n_raw * 96, (const void**)&raw_dev},
-        {b->scalars, b->scalars ? (size_t)n * 8 : 0, (const void**)&d.scalars},
-        {b->sigs, need_sigs ? (size_t)n * 192 : 0, (const void**)&d.sigs},
-        {b->sig_len, need_sigs ? (size_t)n * 4 : 0, (const void**)&d.sig_len},
-    };
-    if (int r = stage_packed(c, segs, 8)) return r;
+    memcpy(c->jo_host.data(), jo, c->jo_host.size() * 4);
+    c->pk_total = total;
+    if (int r = stage_issue(c, bytes)) return r;
     if (!b->scalars) d.scalars = nullptr;
     if (!need_sigs) { d.sigs = nullptr; d.sig_len = nullptr; }
     if (int r = c->raw_conv.ensure(b->n_raw ? b->n_raw : 1)) return r;
@@ -397,14 +437,14 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, std::vector<uin
     if (int r = c->raw_conv.ensure(b->n_raw ? b->n_raw : 1)) return r;
     launch_raw_pks(c->st, b->raw_pks, c->raw_conv.p, b->n_raw);
     d.raw_pks = c->raw_conv.p;
-  }
-  // grid bound of the chunked pubkey gather: sum ceil(k_i/32) <= total/32 + n
-  uint32_t total = 0;
-  if (!b->on_device) total = b->pk_offsets[n];
-  else if (n) {
-    HIPCHK(hipMemcpyAsync(&total, b->pk_offsets + n, 4, hipMemcpyDeviceToHost, c->st));
+    // offsets live in HBM: the host needs the job offsets (stats) and the key total (grid bound)
+    HIPCHK(hipMemcpyAsync(c->jo_host.data(), b->job_offsets, c->jo_host.size() * 4, hipMemcpyDeviceToHost, c->st));
+    c->pk_total = 0;
+    if (n) HIPCHK(hipMemcpyAsync(&c->pk_total, b->pk_offsets + n, 4, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
   }
+  const uint32_t total = c->pk_total;
+  // grid bound of the chunked pubkey gather: sum ceil(k_i/32) <= total/32 + n
   d.chunk_bound = total / 32 + n;
   // two pairs per Miller work item only when the batch alone fills the chip
   // (>= 65536 sets ~ 2 waves per SIMD at 1 pair per lane); below that the
@@ -437,7 +477,6 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, std::vector<uin
   } else {
     // fresh 64-bit multipliers on the device: ChaCha20 keyed by 32 bytes of
     // getrandom() (+ 12-byte nonce) per call, rng.h
-    (void)scal_host;
     uint32_t kn[11];
     random_bytes(kn, sizeof kn);
     if (int r = c->scalars.ensure(n ? n : 1)) return r;
@@ -461,7 +500,7 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
       (r = c->rsig.ensure(ns)) || (r = c->f_set.ensure(ns + nj)) || (r = c->set_code.ensure(ns)) ||
       (r = c->set_job.ensure(ns)) || (r = c->item_off.ensure(nj + 1)) || (r = c->item_job.ensure(ns + nj + 1)) || (r = c->f_job.ensure(nj)) || (r = c->f_batch.ensure(nj)) || (r = c->f_tmp.ensure(nj / 32 + 1)) ||
       (r = c->s_aff.ensure(nj)) || (r = c->s_inf.ensure(nj)) || (r = c->job_code.ensure(nj)) ||
-      (r = c->job_result.ensure(nj)) || (r = c->f_part.ensure(4)) || (r = c->flags.ensure(4)))
+      (r = c->job_result.ensure(nj)) || (r = c->f_part.ensure(4)) || (r = c->flags.ensure(8)))
     return r;
   w.sig_aff = c->sig_aff.p; w.h_aff = c->h_aff.p; w.sig_inf = c->sig_inf.p; w.sig_code = c->sig_code.p;
   w.pk_code = c->pk_code.p; w.rpk_aff = c->rpk_aff.p; w.rsig = c->rsig.p; w.f_set = c->f_set.p;
@@ -469,7 +508,7 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
   w.f_part = c->f_part.p; w.flags = c->flags.p;
   w.item_off = c->item_off.p; w.item_job = c->item_job.p;
   w.set_job = c->set_job.p; w.f_batch = c->f_batch.p; w.f_tmp = c->f_tmp.p; w.s_aff = c->s_aff.p; w.s_inf = c->s_inf.p;
-  w.q_part = nullptr; w.sig_grp = nullptr;
+  w.q_part = nullptr; w.sig_grp = nullptr; w.pk_agg = nullptr;
   if (d.split) {
     if ((r = c->q_part.ensure(2 * ns)) || (r = c->sig_grp.ensure(ns))) return r;
     w.q_part = c->q_part.p; w.sig_grp = c->sig_grp.p;
@@ -487,7 +526,7 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
 // disjoint buffers, bgv_kernels.hip):
 //   st      : sig -> sig_scale -> [pk] sig_sum_tree -> miller_loop_jobs -> [miller] tail
 //   st_hash : hash -> [pk] miller_loop (the set pairs)
-//   st_pk   : pk
+//   st_pk   : pk_gather -> pk_aggregate_scale   ([pk] = after pk_aggregate_scale)
 // The set-pair Miller loops need only H(m) and the aggregated keys, so they
 // start while the signatures are still being scaled: at C4 the Miller kernel
 // fills 78% of the SIMDs (one wave each) and sig_scale takes the rest.
@@ -498,6 +537,8 @@ static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int fro
   const bool fork = c->overlap && from <= ST_SIG && to > ST_F_TREE;
   const bool timed = c->timing >= 0 ? c->timing != 0 : d.n_sets >= 65536;
   c->timed = timed;
+  c->run_from = from;
+  c->run_to = to;
   hipEvent_t* dep = timed ? c->ev_end : c->ev_dep;  // what the stream waits below wait on
   if (!timed) HIPCHK(hipEventRecord(c->ev[from], c->st));
   // latency batches fork the hash leg BEFORE the index set-up: hash_to_G2 reads
@@ -509,19 +550,15 @@ static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int fro
     hipStream_t st = c->st;
     if (fork) {
       if (s == ST_HASH || s == ST_MILLER) st = c->st_hash;
-      if (s == ST_PK) st = c->st_pk;
-      if (s == ST_S_TREE || s == ST_MILLER) HIPCHK(hipStreamWaitEvent(st, dep[ST_PK], 0));
+      if (s == ST_PK || s == ST_PK_SCALE) st = c->st_pk;
+      if (s == ST_S_TREE || s == ST_MILLER) HIPCHK(hipStreamWaitEvent(st, dep[ST_PK_SCALE], 0));
       if (s == ST_F_TREE) HIPCHK(hipStreamWaitEvent(st, dep[ST_MILLER], 0));
-      // A/B knobs: hold the signature leg back so hash/pk (the Miller inputs) get the chip first
-      if (s == ST_SIG_SCALE && (c->sched & 1)) HIPCHK(hipStreamWaitEvent(st, dep[ST_HASH], 0));
-      if (s == ST_SIG && (c->sched & 2)) HIPCHK(hipStreamWaitEvent(st, dep[ST_HASH], 0));
-      if (s == ST_SIG_SCALE && (c->sched & 4)) HIPCHK(hipStreamWaitEvent(st, dep[ST_PK], 0));
     }
     if (timed) HIPCHK(hipEventRecord(c->ev[s], st));
     launch_stage(st, s, d, w);
     HIPCHK(hipGetLastError());
     if (timed) HIPCHK(hipEventRecord(c->ev_end[s], st));
-    else if (fork && (s == ST_PK || s == ST_HASH || s == ST_MILLER)) HIPCHK(hipEventRecord(c->ev_dep[s], st));
+    else if (fork && (s == ST_PK_SCALE || s == ST_HASH || s == ST_MILLER)) HIPCHK(hipEventRecord(c->ev_dep[s], st));
     return 0;
   };
   if (early_hash) {  // enqueued first, so the host's launch latency does not delay it either
@@ -541,25 +578,16 @@ static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int fro
   int order[ST_COUNT], n_order = 0;
   for (int s = from; s < to; s++)
     if (!(early_hash && s == ST_HASH)) order[n_order++] = s;
-  if (fork && (c->sched & 2) && from == ST_SIG && !early_hash) {  // enqueue sig after hash/pk so it can wait on them
-    order[0] = ST_HASH; order[1] = ST_PK; order[2] = ST_SIG;
-  }
   for (int oi = 0; oi < n_order; oi++)
     if (int r = launch_one(order[oi])) return r;
   HIPCHK(hipEventRecord(c->ev[to], c->st));
   return 0;
 }
 
-int bgv_verify(bgv_ctx* c, const bgv_batch* b, int32_t* job_result, int32_t* set_code, bgv_stats* stats) {
-  if (!c || !b || (!job_result && b->n_jobs)) return fail(BGV_E_INVALID_ARG, "null argument");
-  HIPCHK(hipSetDevice(c->device));
-  dev_batch d;
-  std::vector<uint64_t> scal;
-  if (int r = prepare(c, b, d, scal, true)) return r;
-  dev_work w;
-  if (int r = work_alloc(c, d, w)) return r;
-  if (int r = run_stages(c, d, w, 0, ST_COUNT)) return r;
-  // results through pinned memory: [flag | job_result | set_code]
+// job results, set codes and the batch flag through pinned memory; the
+// lodestar_bls_thread_pool_* counters from the host view of the offsets
+static int finish_results(bgv_ctx* c, const dev_batch& d, const dev_work& w, int32_t* job_result, int32_t* set_code,
+                          bgv_stats* stats) {
   const size_t jr_off = 256, sc_off = jr_off + (((size_t)d.n_jobs * 4 + 255) & ~size_t(255));
   const bool want_sc = set_code && d.n_sets;
   if (int r = pinned_reserve(c->pin_out, c->pin_out_cap, sc_off + (want_sc ? (size_t)d.n_sets * 4 : 0))) return r;
@@ -580,24 +608,38 @@ int bgv_verify(bgv_ctx* c, const bgv_batch* b, int32_t* job_result, int32_t* set
     stats->n_sets = d.n_sets;
     stats->n_jobs = d.n_jobs;
     uint32_t valid_jobs = 0, valid_sets = 0;
-    const uint32_t* jo = b->job_offsets;
-    std::vector<uint32_t> jo_host;
-    uint32_t pk_total = 0;
-    if (b->on_device) {  // offsets live in HBM: read them back (4 B per job)
-      jo_host.resize(d.n_jobs + 1);
-      HIPCHK(hipMemcpy(jo_host.data(), b->job_offsets, jo_host.size() * 4, hipMemcpyDeviceToHost));
-      HIPCHK(hipMemcpy(&pk_total, b->pk_offsets + d.n_sets, 4, hipMemcpyDeviceToHost));
-      jo = jo_host.data();
-    } else {
-      pk_total = b->pk_offsets[d.n_sets];
-    }
+    const uint32_t* jo = c->jo_host.data();
     for (uint32_t j = 0; j < d.n_jobs; j++)
       if (job_result[j] >= 0) { valid_jobs++; valid_sets += jo[j + 1] - jo[j]; }
-    stats->pubkeys_aggregated = pk_total;
+    stats->pubkeys_aggregated = c->pk_total;
     stats->batch_retries = (valid_jobs && !flag) ? 1u : 0u;
     stats->batch_sigs_success = flag ? valid_sets : 0u;
   }
+  return 0;
+}
+
+int bgv_last_stats(bgv_ctx* c, bgv_stats* stats) {
+  if (!c || !stats) return fail(BGV_E_INVALID_ARG, "null argument");
+  memset(stats, 0, sizeof *stats);
+  if (c->run_to <= c->run_from) return BGV_OK;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipEventSynchronize(c->ev[c->run_to]));
+  if (c->timed)
+    for (int s = c->run_from; s < c->run_to && s < BGV_N_STAGES; s++) HIPCHK(hipEventElapsedTime(&stats->stage_ms[s], c->ev[s], c->ev_end[s]));
+  HIPCHK(hipEventElapsedTime(&stats->total_ms, c->ev[c->run_from], c->ev[c->run_to]));
   return BGV_OK;
+}
+
+int bgv_verify(bgv_ctx* c, const bgv_batch* b, int32_t* job_result, int32_t* set_code, bgv_stats* stats) {
+  if (!c || !b || (!job_result && b->n_jobs)) return fail(BGV_E_INVALID_ARG, "null argument");
+  c->partial_pending = false;
+  HIPCHK(hipSetDevice(c->device));
+  dev_batch d;
+  if (int r = prepare(c, b, d, true)) return r;
+  dev_work w;
+  if (int r = work_alloc(c, d, w)) return r;
+  if (int r = run_stages(c, d, w, 0, ST_COUNT)) return r;
+  return finish_results(c, d, w, job_result, set_code, stats);
 }
 
 // ---- multi-GPU partials ---------------------------------------------------
@@ -618,12 +660,13 @@ static void fp12_plain_from_bytes(fp12_t& f, const uint8_t* in) {
   }
 }
 
-int bgv_partial(bgv_ctx* c, const bgv_batch* b, uint8_t* miller576, int32_t* set_code, int32_t* ok_out) {
+int bgv_partial(bgv_ctx* c, const bgv_batch* b, uint8_t* miller576, int32_t* set_code, int32_t* job_result,
+                int32_t* ok_out) {
   if (!c || !b || !miller576) return fail(BGV_E_INVALID_ARG, "null argument");
+  c->partial_pending = false;
   HIPCHK(hipSetDevice(c->device));
   dev_batch d;
-  std::vector<uint64_t> scal;
-  if (int r = prepare(c, b, d, scal, true)) return r;
+  if (int r = prepare(c, b, d, true)) return r;
   dev_work w;
   if (int r = work_alloc(c, d, w)) return r;
   if (int r = run_stages(c, d, w, ST_SIG, ST_BATCH_FINAL)) return r;
@@ -641,36 +684,128 @@ int bgv_partial(bgv_ctx* c, const bgv_batch* b, uint8_t* miller576, int32_t* set
   if (d.n_jobs) HIPCHK(hipMemcpyAsync(jc.data(), w.job_code, (size_t)d.n_jobs * 4, hipMemcpyDeviceToHost, c->st));
   if (set_code && d.n_sets) HIPCHK(hipMemcpyAsync(set_code, w.set_code, (size_t)d.n_sets * 4, hipMemcpyDeviceToHost, c->st));
   HIPCHK(hipStreamSynchronize(c->st));
+  c->staged_pending = false;
   fp12_plain_to_bytes(miller576, f);
   int32_t ok = 1;
-  for (uint32_t j = 0; j < d.n_jobs; j++)
+  for (uint32_t j = 0; j < d.n_jobs; j++) {
     if (jc[j] != 0) ok = 0;
+    if (job_result) job_result[j] = jc[j] != 0 ? -jc[j] : 1;
+  }
   if (ok_out) *ok_out = ok;
+  c->part_d = d;
+  c->part_w = w;
+  c->partial_pending = true;
   return BGV_OK;
 }
 
+int bgv_partial_finish(bgv_ctx* c, int32_t* job_result, bgv_stats* stats) {
+  if (!c) return fail(BGV_E_INVALID_ARG, "null ctx");
+  if (!c->partial_pending) return fail(BGV_E_STATE, "bgv_partial_finish needs bgv_partial as the previous call on the context");
+  const dev_batch& d = c->part_d;
+  const dev_work& w = c->part_w;
+  if (!job_result && d.n_jobs) return fail(BGV_E_INVALID_ARG, "null argument");
+  c->partial_pending = false;
+  HIPCHK(hipSetDevice(c->device));
+  c->timed = false;
+  c->run_from = 0;
+  c->run_to = ST_COUNT;
+  HIPCHK(hipEventRecord(c->ev[0], c->st));
+  launch_stage(c->st, ST_BATCH_FINAL, d, w);
+  launch_stage(c->st, ST_JOB_FINAL, d, w);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev[ST_COUNT], c->st));
+  return finish_results(c, d, w, job_result, nullptr, stats);
+}
+
+// (keeps a pending bgv_partial state: the dist flow is partial -> combine ->
+// partial_finish; the combination touches only f_part and its own flag word)
 int bgv_combine_final(bgv_ctx* c, const uint8_t* parts, uint32_t n, int32_t* is_one) {
   if (!c || (!parts && n) || !is_one) return fail(BGV_E_INVALID_ARG, "null argument");
   HIPCHK(hipSetDevice(c->device));
   std::vector<fp12_t> h(n ? n : 1);
   for (uint32_t k = 0; k < n; k++) fp12_plain_from_bytes(h[k], parts + 576u * k);
   if (int r = c->f_part.ensure(2 * (size_t)n + 65)) return r;
-  if (int r = c->flags.ensure(4)) return r;
+  if (int r = c->flags.ensure(8)) return r;
   if (n) HIPCHK(hipMemcpyAsync(c->f_part.p + n, h.data(), (size_t)n * sizeof(fp12_t), hipMemcpyHostToDevice, c->st));
   launch_fp12_convert(c->st, c->f_part.p + n, c->f_part.p, n, true);
-  launch_combine_final(c->st, c->f_part.p, n, c->flags.p);
+  launch_combine_final(c->st, c->f_part.p, n, c->flags.p + 4);
   HIPCHK(hipGetLastError());
   uint32_t flag = 0;
-  HIPCHK(hipMemcpyAsync(&flag, c->flags.p, 4, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipMemcpyAsync(&flag, c->flags.p + 4, 4, hipMemcpyDeviceToHost, c->st));
   HIPCHK(hipStreamSynchronize(c->st));
   *is_one = flag ? 1 : 0;
+  return BGV_OK;
+}
+
+// ---- test-only: per-stage intermediates -------------------------------------
+int bgv_debug_stages(bgv_ctx* c, const bgv_batch* b, int32_t* job_result, int32_t* set_code, bgv_debug* o) {
+  if (!c || !b || !o || (!job_result && b->n_jobs)) return fail(BGV_E_INVALID_ARG, "null argument");
+  c->partial_pending = false;
+  HIPCHK(hipSetDevice(c->device));
+  dev_batch d;
+  if (int r = prepare(c, b, d, true)) return r;
+  dev_work w;
+  if (int r = work_alloc(c, d, w)) return r;
+  const uint32_t n = d.n_sets, J = d.n_jobs;
+  if (int r = c->pk_agg.ensure(n ? n : 1)) return r;
+  w.pk_agg = c->pk_agg.p;
+  if (int r = run_stages(c, d, w, 0, ST_COUNT)) return r;
+  // final exponentiations of every Miller value, job product and the batch product
+  const uint32_t n_fe = n + 2 * J + 1;
+  if (int r = c->dbg_fe.ensure(n_fe)) return r;
+  launch_final_exp_many(c->st, w.f_set, c->dbg_fe.p, n + J);
+  launch_final_exp_many(c->st, w.f_job, c->dbg_fe.p + n + J, J);
+  if (J) launch_final_exp_many(c->st, w.f_batch, c->dbg_fe.p + n + 2 * J, 1);
+  launch_fp12_convert(c->st, c->dbg_fe.p, c->dbg_fe.p, n_fe, false);
+  HIPCHK(hipGetLastError());
+  struct part { uint8_t* host; size_t bytes; } parts[8];
+  int np = 0;
+  size_t off = 0;
+  auto add = [&](uint8_t* host, size_t bytes) -> uint8_t* {
+    const size_t o2 = off;
+    off += (bytes + 255) & ~size_t(255);
+    parts[np++] = {host, bytes};
+    return (uint8_t*)o2;  // offset, rebased below
+  };
+  uint8_t* o_sig = add(o->sig_aff, (size_t)n * 192);
+  uint8_t* o_h = add(o->h_aff, (size_t)n * 192);
+  uint8_t* o_pk = add(o->pk_agg, (size_t)n * 96);
+  uint8_t* o_rpk = add(o->rpk_aff, (size_t)n * 96);
+  uint8_t* o_s = add(o->s_aff, (size_t)J * 192);
+  if (int r = c->dbg_out.ensure(off ? off : 1)) return r;
+  uint8_t* base = c->dbg_out.p;
+  launch_export_g2a(c->st, w.sig_aff, base + (size_t)o_sig, n);
+  launch_export_g2a(c->st, w.h_aff, base + (size_t)o_h, n);
+  launch_export_g1a(c->st, w.pk_agg, base + (size_t)o_pk, n);
+  launch_export_g1a(c->st, w.rpk_aff, base + (size_t)o_rpk, n);
+  launch_export_g2a(c->st, w.s_aff, base + (size_t)o_s, J);
+  HIPCHK(hipGetLastError());
+  size_t pos = 0;
+  for (int k = 0; k < np; k++) {
+    if (parts[k].host && parts[k].bytes) HIPCHK(hipMemcpyAsync(parts[k].host, base + pos, parts[k].bytes, hipMemcpyDeviceToHost, c->st));
+    pos += (parts[k].bytes + 255) & ~size_t(255);
+  }
+  std::vector<fp12_t> fe(n_fe);
+  HIPCHK(hipMemcpyAsync(fe.data(), c->dbg_fe.p, (size_t)n_fe * sizeof(fp12_t), hipMemcpyDeviceToHost, c->st));
+  if (int r = finish_results(c, d, w, job_result, set_code, nullptr)) return r;
+  if (o->pair_fe)
+    for (uint32_t k = 0; k < n + J; k++) fp12_plain_to_bytes(o->pair_fe + 576u * k, fe[k]);
+  if (o->job_fe)
+    for (uint32_t k = 0; k < J; k++) fp12_plain_to_bytes(o->job_fe + 576u * k, fe[n + J + k]);
+  if (o->batch_fe) {
+    if (J) fp12_plain_to_bytes(o->batch_fe, fe[n + 2 * J]);
+    else memset(o->batch_fe, 0, 576);
+  }
   return BGV_OK;
 }
 
 // ---- synthetic data --------------------------------------------------------
 int bgv_gen_keys(bgv_ctx* c, uint32_t first, uint32_t n, uint64_t seed) {
   if (!c) return fail(BGV_E_INVALID_ARG, "null ctx");
+  c->partial_pending = false;
   if (n == 0) return BGV_OK;
+  if ((uint64_t)first + n > TABLE_MAX) return fail(BGV_E_TABLE_RANGE, "rows [%u, %llu) exceed the table limit 2^31 - 1", first, (unsigned long long)first + n);
+  if (first > c->table_n) return fail(BGV_E_TABLE_RANGE, "row %u would leave a gap after the %u rows of the table", first, c->table_n);
   HIPCHK(hipSetDevice(c->device));
   if (int r = table_reserve(c, first + n)) return r;
   if (c->sk.cap < (size_t)(first + n) * 8) {
@@ -694,11 +829,11 @@ int bgv_gen_sign(bgv_ctx* c, const bgv_batch* b, uint8_t* sigs_out) {
   if (!c || !b || !sigs_out) return fail(BGV_E_INVALID_ARG, "null argument");
   if (!c->sk.p) return fail(BGV_E_INVALID_ARG, "bgv_gen_keys has not run on this context");
   HIPCHK(hipSetDevice(c->device));
+  c->partial_pending = false;
   dev_batch d;
-  std::vector<uint64_t> scal;
   bgv_batch bb = *b;
   bb.scalars = nullptr;
-  if (int r = prepare(c, &bb, d, scal, false)) return r;
+  if (int r = prepare(c, &bb, d, false)) return r;
   uint8_t* out = sigs_out;
   if (!b->on_device) {
     if (int r = c->gen_out.ensure((size_t)d.n_sets * 192 + 1)) return r;

@@ -49,6 +49,7 @@ struct dev_work {
   uint32_t* chunk_set;  // set of every chunk
   g1j* pk_part;         // per-chunk partial sums
   g1a* rpk_aff;       // [r_i] aggregated pubkey, affine
+  g1a* pk_agg;        // aggregated pubkey before scaling, affine (bgv_debug_stages only; else NULL)
   int32_t* pk_code;
   g2j* rsig;          // [r_i] sigma_i
   uint32_t* set_job;  // job id of every set
@@ -70,7 +71,8 @@ struct dev_work {
 enum Stage {
   ST_SIG = 0,
   ST_HASH,
-  ST_PK,
+  ST_PK,        // chunked gather + partial sums from the HBM table (k_pk_chunk)
+  ST_PK_SCALE,  // per set: fold the chunk sums, [r_i] PK_i, affine (k_pk)
   ST_SIG_SCALE,
   ST_S_TREE,
   ST_MILLER,
@@ -84,8 +86,8 @@ enum Stage {
 };
 
 void launch_raw_pks(hipStream_t st, const uint8_t* raw, g1a* out, uint32_t n);
-void launch_table_from_compressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n);
-void launch_table_from_uncompressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n);
+void launch_table_from_compressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n, int32_t* codes);
+void launch_table_from_uncompressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n, int32_t* codes);
 void launch_table_export(hipStream_t st, const g1a* tab, uint8_t* out, uint32_t n);
 void launch_pk_validate(hipStream_t st, const uint8_t* in, uint32_t n, int32_t* codes);
 void launch_prep(hipStream_t st, const dev_batch& b, const dev_work& w);  // before ST_PK / ST_MILLER
@@ -95,6 +97,9 @@ void launch_sig_split_coop(hipStream_t st, const dev_batch& b, const dev_work& w
 void launch_hash_clear_coop(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_latency.hip
 void launch_fp12_tail(hipStream_t st, int stage, const dev_batch& b, const dev_work& w);  // bgv_tail.hip
 void launch_combine_final(hipStream_t st, const fp12_t* parts, uint32_t n, uint32_t* flag);
+void launch_final_exp_many(hipStream_t st, const fp12_t* in, fp12_t* out, uint32_t n);  // bgv_debug_stages
+void launch_export_g1a(hipStream_t st, const g1a* in, uint8_t* out96, uint32_t n);
+void launch_export_g2a(hipStream_t st, const g2a* in, uint8_t* out192, uint32_t n);
 void launch_fp12_convert(hipStream_t st, const fp12_t* in, fp12_t* out, uint32_t n, bool to_mont);
 void launch_gen_keys(hipStream_t st, g1a* table, uint32_t* sk, uint32_t first, uint32_t n, uint64_t seed);
 void launch_gen_sign(hipStream_t st, const dev_batch& b, const uint32_t* sk, uint8_t* out);

@@ -102,22 +102,60 @@ __global__ void BGV_BULK k_raw_pks(const uint8_t* raw, g1a* out, uint32_t n) {
   out[i] = p;
 }
 
-// compressed 48 B table load (syncPubkeys path); bad keys -> (0, 0)
-__global__ void BGV_BULK k_table_from_compressed(const uint8_t* in48, g1a* out, uint32_t n) {
+// compressed 48 B table load (syncPubkeys path: PublicKey.fromBytes(pk,
+// jacobian) without validation, pubkeyCache.ts:75): decode + on-curve, the
+// infinity key is stored as (0, 0) and adds nothing to an aggregate; codes[i]
+// is the blst code of a key that does not decode (the host rejects the call)
+__global__ void BGV_BULK k_table_from_compressed(const uint8_t* in48, g1a* out, uint32_t n, int32_t* codes) {
   const uint32_t i = gtid();
   if (i >= n) return;
   g1a p;
   bool inf;
-  if (g1_decompress(p, inf, in48 + 48u * i) != C_OK || inf) { fp_set_zero(p.x); fp_set_zero(p.y); }
+  const int32_t c = g1_decompress(p, inf, in48 + 48u * i);
+  if (c != C_OK || inf) { fp_set_zero(p.x); fp_set_zero(p.y); }
   out[i] = p;
+  codes[i] = c;
 }
 
-__global__ void BGV_BULK k_table_from_uncompressed(const uint8_t* in96, g1a* out, uint32_t n) {
+// 96 B uncompressed (x || y big-endian): blst deserialization checks the
+// flags, x, y < p and the curve equation (no subgroup check)
+__global__ void BGV_BULK k_table_from_uncompressed(const uint8_t* in96, g1a* out, uint32_t n, int32_t* codes) {
   const uint32_t i = gtid();
   if (i >= n) return;
+  const uint8_t* b = in96 + 96u * i;
   g1a p;
-  if (!g1_from_uncompressed_trusted(p, in96 + 96u * i)) { fp_set_zero(p.x); fp_set_zero(p.y); }
+  fp_set_zero(p.x);
+  fp_set_zero(p.y);
+  int32_t c = C_OK;
+  if (b[0] & 0x80) {
+    c = C_BAD_ENCODING;  // compressed flag on a 96-byte key
+  } else if (b[0] & 0x40) {  // infinity: every other bit zero
+    uint32_t acc = b[0] & 0x3f;
+    for (int k = 1; k < 96; k++) acc |= b[k];
+    if (acc) c = C_BAD_ENCODING;
+  } else {
+    fp_t x, y;
+    fp_from_be48(x, b);
+    fp_from_be48(y, b + 48);
+    if ((b[0] & 0x20) || !fp_plain_lt_p(x) || !fp_plain_lt_p(y)) {
+      c = C_BAD_ENCODING;
+    } else {
+      fp_to_mont(p.x, x);
+      fp_to_mont(p.y, y);
+      fp_t y2, x3;
+      fp_sqr(y2, p.y);
+      fp_sqr(x3, p.x);
+      fp_mul(x3, x3, p.x);
+      fp_add(x3, x3, B1_MONT);
+      if (!fp_eq(y2, x3)) {
+        c = C_POINT_NOT_ON_CURVE;
+        fp_set_zero(p.x);
+        fp_set_zero(p.y);
+      }
+    }
+  }
   out[i] = p;
+  codes[i] = c;
 }
 
 __global__ void BGV_BULK k_table_export(const g1a* tab, uint8_t* out96, uint32_t n) {
@@ -135,6 +173,31 @@ __global__ void BGV_BULK k_table_export(const g1a* tab, uint8_t* out96, uint32_t
   fp_to_be48(o, t);
   fp_from_mont(t, p.y);
   fp_to_be48(o + 48, t);
+}
+
+// plain big-endian export of affine points (bgv_debug_stages): x then y,
+// Fp2 coordinates as c0 || c1; the identity (0, 0) stays all-zero
+__global__ void BGV_BULK k_export_g1a(const g1a* in, uint8_t* out96, uint32_t n) {
+  const uint32_t i = gtid();
+  if (i >= n) return;
+  const g1a p = in[i];
+  fp_t t;
+  fp_from_mont(t, p.x);
+  fp_to_be48(out96 + 96u * i, t);
+  fp_from_mont(t, p.y);
+  fp_to_be48(out96 + 96u * i + 48, t);
+}
+
+__global__ void BGV_BULK k_export_g2a(const g2a* in, uint8_t* out192, uint32_t n) {
+  const uint32_t i = gtid();
+  if (i >= n) return;
+  const g2a p = in[i];
+  const fp_t* c[4] = {&p.x.c0, &p.x.c1, &p.y.c0, &p.y.c1};
+  for (int k = 0; k < 4; k++) {
+    fp_t t;
+    fp_from_mont(t, *c[k]);
+    fp_to_be48(out192 + 192u * i + 48 * k, t);
+  }
 }
 
 // ------------------------------------------------------------------ k_sig
@@ -275,10 +338,14 @@ __global__ void __launch_bounds__(64, BGV_HASH_WAVES) k_hash(dev_batch b, dev_wo
 // chunk sums, applies the batch scalar r_i and converts to affine.
 constexpr uint32_t PK_CHUNK = 32;
 
+// Offsets that run backwards (an on-device batch that breaks the contract;
+// host batches are checked by the library) give the set no chunks, and the
+// chunk scan is clipped at chunk_bound below: no access leaves the buffers.
 __global__ void BGV_BULK k_chunk_count(dev_batch b, dev_work w) {
   const uint32_t i = gtid();
   if (i >= b.n_sets) return;
-  const uint32_t k = b.pk_off[i + 1] - b.pk_off[i];
+  const uint32_t lo = b.pk_off[i], hi = b.pk_off[i + 1];
+  const uint32_t k = hi > lo ? hi - lo : 0u;
   w.chunk_off[i] = (k + PK_CHUNK - 1) / PK_CHUNK;
 }
 
@@ -320,7 +387,8 @@ __global__ void __launch_bounds__(1024) k_scan(uint32_t* a, uint32_t n) {
 __global__ void BGV_BULK k_chunk_set(dev_batch b, dev_work w) {
   const uint32_t i = gtid();
   if (i >= b.n_sets) return;
-  for (uint32_t c = w.chunk_off[i]; c < w.chunk_off[i + 1]; c++) w.chunk_set[c] = i;
+  const uint32_t end = min(w.chunk_off[i + 1], b.chunk_bound);
+  for (uint32_t c = w.chunk_off[i]; c < end; c++) w.chunk_set[c] = i;
 }
 
 #ifndef BGV_PKC_WAVES
@@ -328,7 +396,7 @@ __global__ void BGV_BULK k_chunk_set(dev_batch b, dev_work w) {
 #endif
 __global__ void __launch_bounds__(64, BGV_PKC_WAVES) k_pk_chunk(dev_batch b, dev_work w) {
   const uint32_t g = gtid();
-  if (g >= w.chunk_off[b.n_sets]) return;
+  if (g >= min(w.chunk_off[b.n_sets], b.chunk_bound)) return;
   const uint32_t i = w.chunk_set[g];
   const uint32_t beg = b.pk_off[i] + (g - w.chunk_off[i]) * PK_CHUNK;
   const uint32_t end = min(beg + PK_CHUNK, b.pk_off[i + 1]);
@@ -354,8 +422,9 @@ __global__ void __launch_bounds__(64, BGV_PK_WAVES) k_pk(dev_batch b, dev_work w
   if (i >= b.n_sets) return;
   g1j acc;
   jac_set_inf(acc);
-  bool range_err = false;
-  for (uint32_t c = w.chunk_off[i]; c < w.chunk_off[i + 1]; c++) {
+  const uint32_t c0 = w.chunk_off[i], c1 = w.chunk_off[i + 1];
+  bool range_err = c1 > b.chunk_bound || b.pk_off[i + 1] < b.pk_off[i];
+  for (uint32_t c = c0; c < c1 && !range_err; c++) {
     const g1j p = w.pk_part[c];
     if (!jac_is_inf(p) && fp_is_zero(p.x)) range_err = true;
     jac_add(acc, acc, p);
@@ -364,6 +433,10 @@ __global__ void __launch_bounds__(64, BGV_PK_WAVES) k_pk(dev_batch b, dev_work w
   if (range_err) code = C_INDEX_RANGE;
   else if (jac_is_inf(acc)) code = C_PK_IS_INFINITY;
   g1a out;
+  if (w.pk_agg) {  // bgv_debug_stages: the aggregate before scaling
+    if (code != C_OK || !jac_to_aff(out, acc)) { fp_set_zero(out.x); fp_set_zero(out.y); }
+    w.pk_agg[i] = out;
+  }
   if (code == C_OK) {
     g1j rp;
     jac_mul_u64_w4(rp, acc, b.scalars[i]);
@@ -532,7 +605,8 @@ __global__ void BGV_BULK k_job_s(dev_batch b, dev_work w, uint32_t span) {
 __global__ void BGV_BULK k_item_count(dev_batch b, dev_work w) {
   const uint32_t j = gtid();
   if (j >= b.n_jobs) return;
-  w.item_off[j] = (b.job_off[j + 1] - b.job_off[j] + b.pairs_per_item - 1) / b.pairs_per_item;
+  const uint32_t lo = b.job_off[j], hi = b.job_off[j + 1];
+  w.item_off[j] = hi > lo ? (hi - lo + b.pairs_per_item - 1) / b.pairs_per_item : 0u;
 }
 
 __global__ void BGV_BULK k_item_job(dev_batch b, dev_work w) {
@@ -541,8 +615,7 @@ __global__ void BGV_BULK k_item_job(dev_batch b, dev_work w) {
   for (uint32_t t = w.item_off[j]; t < w.item_off[j + 1]; t++) w.item_job[t] = j;
 }
 
-// k_miller (the set-pair Miller loops) lives in bgv_miller.hip: that unit
-// uses the Fp2 product leaf with lazy reduction (fp2.h BGV_FP2_LEAF).
+// k_miller (the set-pair Miller loops) lives in bgv_miller.hip (1 wave/SIMD).
 
 // Cooperative variant (miller_coop.h): COOP_GROUPS pairs per 64-lane
 // workgroup, 6 x COOP_SUB lanes per pair, pair t < n_sets is (r_t PK_t, H(m_t)), then (-G1, S_job).
@@ -800,12 +873,14 @@ static inline dim3 grid64(uint32_t n) { return dim3((n + 63u) / 64u); }
   } while (0)
 
 void launch_raw_pks(hipStream_t st, const uint8_t* raw, g1a* out, uint32_t n) { BGV_LAUNCH(k_raw_pks, n, raw, out, n); }
-void launch_table_from_compressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n) {
-  BGV_LAUNCH(k_table_from_compressed, n, in, out, n);
+void launch_table_from_compressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n, int32_t* codes) {
+  BGV_LAUNCH(k_table_from_compressed, n, in, out, n, codes);
 }
-void launch_table_from_uncompressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n) {
-  BGV_LAUNCH(k_table_from_uncompressed, n, in, out, n);
+void launch_table_from_uncompressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n, int32_t* codes) {
+  BGV_LAUNCH(k_table_from_uncompressed, n, in, out, n, codes);
 }
+void launch_export_g1a(hipStream_t st, const g1a* in, uint8_t* out96, uint32_t n) { BGV_LAUNCH(k_export_g1a, n, in, out96, n); }
+void launch_export_g2a(hipStream_t st, const g2a* in, uint8_t* out192, uint32_t n) { BGV_LAUNCH(k_export_g2a, n, in, out192, n); }
 void launch_pk_validate(hipStream_t st, const uint8_t* in, uint32_t n, int32_t* codes) {
   BGV_LAUNCH(k_pk_validate, n, in, n, codes);
 }
@@ -856,15 +931,16 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
         BGV_LAUNCH(k_hash, b.n_sets, b, w);
       }
       break;
-    case ST_PK:  // after launch_prep
+    case ST_PK:  // after launch_prep: the gather from the HBM table
       BGV_LAUNCH(k_pk_chunk, b.chunk_bound, b, w);
+      break;
+    case ST_PK_SCALE:
       BGV_LAUNCH(k_pk, b.n_sets, b, w);
       break;
     case ST_SIG_SCALE:
       if (b.split && !b.msm) break;  // [r_i] sigma_i already ran in k_sig_split
       if (b.msm) {
         BGV_LAUNCH(k_msm_bucket, b.n_jobs * 16u, b, w);
-        BGV_LAUNCH(k_msm_window, b.n_jobs * 16u, b, w);
       } else {
         BGV_LAUNCH(k_sig_scale, b.n_sets, b, w);
       }
@@ -872,6 +948,7 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
     case ST_S_TREE:
       BGV_LAUNCH(k_set_job, b.n_jobs, b, w);
       if (b.msm) {
+        BGV_LAUNCH(k_msm_window, b.n_jobs * 16u, b, w);
         BGV_LAUNCH(k_msm_job, b.n_jobs, b, w);
         break;
       }

@@ -1,18 +1,10 @@
-// The set-pair Miller loop kernel (k_miller), in its own translation unit so
-// that its Fp2 products can go through the Fp2 leaf with lazy reduction
-// (BGV_FP2_LEAF=1, fp.h fp2_mul28_lazy: 980 digit products per Fp2 product
-// instead of 3 x 392).  That leaf needs 248 VGPRs, which only this kernel
-// (1 wave/SIMD, 512-register budget) can give it.  Measured on MI355X:
-// k_miller 19.5 ms against 18.8-19.2 ms with the Fp leaf (the 16 operand
-// dwords past v31 travel through scratch and the signed 64-bit column
-// shifts cost hazard NOPs), so the knob is off.
+// The set-pair Miller loop kernel (k_miller), in its own translation unit:
+// it runs at 1 wave/SIMD (512-register budget, spills in AGPRs) with its Fp12
+// accumulator in LDS, which no other kernel of bgv_kernels.hip wants.
 // Work items: every job's sets taken two at a time (one shared Fp12
 // accumulator and squaring per two pairs, miller_loop2), then one item per
 // job for its (-G1, S_job) pair.  Item offsets per job come from a scan
 // (bgv_kernels.hip k_item_count / k_item_job).
-#ifndef BGV_FP2_LEAF
-#define BGV_FP2_LEAF 0
-#endif
 #ifndef BGV_FPMUL_CALL
 #define BGV_FPMUL_CALL 1
 #endif

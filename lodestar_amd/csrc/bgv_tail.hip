@@ -156,6 +156,15 @@ __global__ void COOP_LB k_combine_final(const fp12_t* parts, uint32_t n, uint32_
   if (threadIdx.x == 0) flag[0] = one ? 1u : 0u;
 }
 
+// bgv_debug_stages: out[i] = FE(in[i]) (the cubed value of c_final_exp), one
+// cooperative workgroup per element
+__global__ void COOP_LB k_final_exp_many(const fp12_t* in, fp12_t* out) {
+  __shared__ cscratch s;
+  __shared__ fp12_t r;
+  c_final_exp(&r, in[blockIdx.x], &s);
+  if (threadIdx.x == 0) out[blockIdx.x] = r;
+}
+
 #undef gtid
 
 void launch_fp12_tail(hipStream_t st, int stage, const dev_batch& b, const dev_work& w) {
@@ -194,6 +203,10 @@ void launch_fp12_tail(hipStream_t st, int stage, const dev_batch& b, const dev_w
   } else if (stage == ST_JOB_FINAL) {
     if (b.n_jobs) hipLaunchKernelGGL(k_job_final, dim3(b.n_jobs), ct, 0, st, b, w);
   }
+}
+
+void launch_final_exp_many(hipStream_t st, const fp12_t* in, fp12_t* out, uint32_t n) {
+  if (n) hipLaunchKernelGGL(k_final_exp_many, dim3(n), dim3(COOP_THREADS), 0, st, in, out);
 }
 
 void launch_combine_final(hipStream_t st, const fp12_t* parts, uint32_t n, uint32_t* flag) {

@@ -366,7 +366,11 @@ BGV_NI int32_t g2_decompress(g2a& out, bool& inf, const uint8_t* b) {
   return C_OK;
 }
 
-// 192-byte uncompressed G2 (blst POINTonE2_Deserialize_Z)
+// 192-byte uncompressed G2 (blst POINTonE2_Deserialize_Z behind
+// @chainsafe/blst's Signature.fromBytes: a 192-byte input must not carry the
+// compression flag (P2_Affine rejects len != (in[0] & 0x80 ? 96 : 192)), the
+// infinity flag needs every other bit zero, and any other flag bit is
+// BAD_ENCODING)
 BGV_NI int32_t g2_deserialize(g2a& out, bool& inf, const uint8_t* b) {
   inf = false;
   const uint8_t b0 = b[0];
@@ -379,6 +383,7 @@ BGV_NI int32_t g2_deserialize(g2a& out, bool& inf, const uint8_t* b) {
     out.x = fp2_zero(); out.y = fp2_zero();
     return C_OK;
   }
+  if (b0 & 0x20) return C_BAD_ENCODING;  // a sign bit only exists on compressed encodings
   fp_t x1, x0, y1, y0;
   fp_from_be48(x1, b);
   x1.l[NL - 1] &= 0x1fffffffu;

@@ -330,75 +330,6 @@ BGV_HD void fp_sqr28(fp_t& r, const fp_t& a) {
   fp_reduce_once(r, t);
 }
 
-// ---- Fp2 product with lazy reduction (Karatsuba, 2 reductions for 3 products)
-// c0 = a0 b0 - a1 b1 and c1 = (a0 + a1)(b0 + b1) - a0 b0 - a1 b1 are formed
-// on the unreduced 28-column digit products (signed 64-bit columns), then
-// each gets ONE Montgomery reduction: 3 x 196 + 2 x 196 = 980 digit products
-// instead of 3 x 392.  Inputs canonical (< p).  Column bound: |column| <
-// 3 x 14 x 2^56 (products) + 14 x 2^56 (reduction) + carry < 2^62.
-// Results: c0 in (-p/8, 1.125p), c1 in [0, 1.25p) before the correction
-// (add p when negative, else one conditional subtraction).
-BGV_HD void redc28_signed(fp_t& r, int64_t acc[28]) {
-#pragma unroll
-  for (int i = 0; i < 14; i++) {
-    const uint32_t m = ((uint32_t)acc[i] * P28_INV) & M28;
-#pragma unroll
-    for (int j = 0; j < 14; j++) acc[i + j] += (int64_t)((uint64_t)m * P28[j]);
-    acc[i + 1] += acc[i] >> 28;  // exact: acc[i] = 0 mod 2^28 here
-  }
-  uint32_t d[14];
-  int64_t c = 0;
-#pragma unroll
-  for (int k = 0; k < 14; k++) {
-    const int64_t v = acc[14 + k] + c;
-    d[k] = (uint32_t)v & M28;
-    c = v >> 28;
-  }
-  fp_t t;
-  pack28(t, d);  // value mod 2^384
-  if (c < 0) {   // value in (-p, 0): value + p
-    uint32_t cy = 0;
-#pragma unroll
-    for (int i = 0; i < NL; i++) r.l[i] = addc32(t.l[i], P_MOD.l[i], cy, cy);
-  } else {
-    fp_reduce_once(r, t);
-  }
-}
-
-BGV_HD void fp2_mul28_lazy(fp_t& r0, fp_t& r1, const fp_t& a0, const fp_t& a1, const fp_t& b0, const fp_t& b1) {
-  uint32_t A0[14], A1[14], B0[14], B1[14];
-  unpack28<8>(A0, a0);
-  unpack28<8>(A1, a1);
-  unpack28<0>(B0, b0);
-  unpack28<0>(B1, b1);
-  uint64_t x[28], y[28];
-#pragma unroll
-  for (int k = 0; k < 28; k++) { x[k] = 0; y[k] = 0; }
-#pragma unroll
-  for (int i = 0; i < 14; i++)
-#pragma unroll
-    for (int j = 0; j < 14; j++) {
-      x[i + j] += (uint64_t)A0[i] * B0[j];
-      y[i + j] += (uint64_t)A1[i] * B1[j];
-    }
-  int64_t c0[28], c1[28];
-#pragma unroll
-  for (int k = 0; k < 28; k++) {
-    c0[k] = (int64_t)(x[k] - y[k]);
-    c1[k] = (int64_t)(0ull - x[k] - y[k]);
-  }
-  // (a0 + a1)(b0 + b1) on digit-wise sums (digits < 2^29, products < 2^58):
-  // the digit vectors are linear, so no carry normalisation is needed
-#pragma unroll
-  for (int i = 0; i < 14; i++) {
-    const uint32_t sa = A0[i] + A1[i];  // < 2^29
-#pragma unroll
-    for (int j = 0; j < 14; j++) c1[i + j] += (int64_t)((uint64_t)sa * (B0[j] + B1[j]));  // < 2^58
-  }
-  redc28_signed(r0, c0);
-  redc28_signed(r1, c1);
-}
-
 #if defined(__HIPCC__) && BGV_FPMUL_CALL
 static __device__ __noinline__ fp_vec_t fp_sqr_leaf(fp_vec_t a) {
   fp_t x, r;

@@ -198,55 +198,6 @@ BGV_NI12 void fp12_mul_line(fp12_t& r, const fp12_t& f, const fp2_t& a0, const f
   fp6_add(r.c0, t0, t1);
 }
 
-// Product of two lines l = (a0 + a1 v) + (b1 v) w and l' (same shape):
-// L = X + Y w with X = (a0a0' + xi b1b1', a0a1' + a1a0', a1a1') and
-// Y = (0, a0b1' + a0'b1, a1b1' + a1'b1); Karatsuba: 6 Fp2 products.
-struct line2_t { fp2_t x0, x1, x2, y1, y2; };
-BGV_NI12 void line_mul_line(line2_t& L, const fp2_t& a0, const fp2_t& a1, const fp2_t& b1, const fp2_t& c0,
-                            const fp2_t& c1, const fp2_t& d1) {
-  fp2_t m00, m11, mbb, s, t, u;
-  F6_MUL(m00, a0, c0);
-  F6_MUL(m11, a1, c1);
-  F6_MUL(mbb, b1, d1);
-  fp2_mul_xi(u, mbb);
-  fp2_add(L.x0, m00, u);
-  fp2_add(s, a0, a1);
-  fp2_add(t, c0, c1);
-  F6_MUL(u, s, t);
-  fp2_sub(u, u, m00);
-  fp2_sub(L.x1, u, m11);
-  L.x2 = m11;
-  fp2_add(s, a0, b1);
-  fp2_add(t, c0, d1);
-  F6_MUL(u, s, t);
-  fp2_sub(u, u, m00);
-  fp2_sub(L.y1, u, mbb);
-  fp2_add(s, a1, b1);
-  fp2_add(t, c1, d1);
-  F6_MUL(u, s, t);
-  fp2_sub(u, u, m11);
-  fp2_sub(L.y2, u, mbb);
-}
-
-// f * L (L from line_mul_line, Y's v^0 coefficient zero): Karatsuba over
-// w with Y = v (y1 + y2 v): 6 + 5 + 6 = 17 Fp2 products instead of the
-// 2 x 13 of two fp12_mul_line calls
-BGV_NI12 void fp12_mul_line2(fp12_t& r, const fp12_t& f, const line2_t& L) {
-  fp6_t X, t0, t1, s, u;
-  X.c0 = L.x0; X.c1 = L.x1; X.c2 = L.x2;
-  fp6_mul(t0, f.c0, X);
-  fp6_mul_01(u, f.c1, L.y1, L.y2);
-  fp6_mul_v(t1, u);  // F1 * Y
-  fp6_add(s, f.c0, f.c1);
-  fp2_add(X.c1, L.x1, L.y1);
-  fp2_add(X.c2, L.x2, L.y2);
-  fp6_mul(s, s, X);
-  fp6_sub(s, s, t0);
-  fp6_sub(r.c1, s, t1);
-  fp6_mul_v(t1, t1);
-  fp6_add(r.c0, t0, t1);
-}
-
 BGV_NI void fp12_inv(fp12_t& r, const fp12_t& a) {
   // 1 / (a0 + a1 w) = (a0 - a1 w) / (a0^2 - v a1^2)
   fp6_t t0, t1;

@@ -208,98 +208,24 @@ __device__ void c_frob(wfp12* out, const wfp12* a, int k, cscratch* s) {
   __syncthreads();
 }
 
-// out = a^2 for a in the cyclotomic subgroup (Granger-Scott, as
-// fp12_cyclotomic_sqr): Fp12 = Fp4[t]/(t^3 - s), s = w^3, A = (g0, g3),
-// B = (g1, g4), C = (g2, g5); A' = 3A^2 - 2 conj(A), B' = 3 s C^2 + 2 conj(B),
-// C' = 3 B^2 - 2 conj(C).  Two rounds instead of c_mul's three:
-//   round 1  lane l < 18: Fp4 f = l / 6, square k = (l % 6) / 2 of
-//            (x_f^2, y_f^2, (x_f + y_f)^2), Fp product l % 2 of the complex
-//            squaring ((u0 + u1)(u0 - u1) | u0 u1)
-//   round 2  lane l < 12: component l % 2 of output coefficient l / 2
-// out may alias a (each round-2 lane reads and writes only its component).
-__device__ void c_cyc_sqr(wfp12* out_, const wfp12* a_, cscratch* s_) {
-  // every operand lives in LDS (lds.h)
-  BGV_LDS wfp12* out = (BGV_LDS wfp12*)out_;
-  const BGV_LDS wfp12* a = (const BGV_LDS wfp12*)a_;
-  BGV_LDS cscratch* s = (BGV_LDS cscratch*)s_;
-  auto get2 = [](const BGV_LDS fp2_t* p) { fp2_t r; r.c0 = lds_get(&p->c0); r.c1 = lds_get(&p->c1); return r; };
-  const uint32_t l = threadIdx.x;
-  if (l < 18) {
-    const uint32_t f = l / 6, r = l - 6 * f, k = r >> 1, comp = r & 1;
-    fp2_t x;
-    if (k == 0) x = get2(&a->c[f]);
-    else if (k == 1) x = get2(&a->c[f + 3]);
-    else fp2_add(x, get2(&a->c[f]), get2(&a->c[f + 3]));
-    fp_t u, v;
-    if (comp == 0) {
-      fp_add_lazy(u, x.c0, x.c1);  // < 2p, product input only
-      fp_sub(v, x.c0, x.c1);
-    } else {
-      u = x.c0;
-      v = x.c1;
-    }
-    fp_t pr;
-    fp_mul(pr, u, v);
-    lds_put(&s->p[l], pr);
-  }
-  __syncthreads();
-  if (l < 12) {
-    const uint32_t j = l >> 1, comp = l & 1;
-    // source Fp4 of output coefficient j: A -> (0, 3), B^2 -> (2, 5), C^2 -> (1, 4)
-    const uint32_t f = (j == 0 || j == 3) ? 0u : ((j == 2 || j == 5) ? 1u : 2u);
-    fp2_t S[3];
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      S[k].c0 = lds_get(&s->p[6 * f + 2 * k]);
-      fp_dbl(S[k].c1, lds_get(&s->p[6 * f + 2 * k + 1]));
-    }
-    fp2_t T0, T1, t;
-    fp2_mul_xi(t, S[1]);
-    fp2_add(T0, S[0], t);        // x^2 + xi y^2
-    fp2_sub(T1, S[2], S[0]);
-    fp2_sub(T1, T1, S[1]);       // 2 x y
-    fp2_t V;
-    if (j == 0 || j == 2 || j == 4) V = T0;
-    else if (j == 1) fp2_mul_xi(V, T1);
-    else V = T1;
-    const fp_t& v = comp ? V.c1 : V.c0;
-    const fp_t g = lds_get(comp ? &a->c[j].c1 : &a->c[j].c0);
-    fp_t v3, g2, r;
-    fp_add(v3, v, v);
-    fp_add(v3, v3, v);
-    fp_dbl(g2, g);
-    if (j & 1) fp_add(r, v3, g2);
-    else fp_sub(r, v3, g2);
-    lds_put(comp ? &out->c[j].c1 : &out->c[j].c0, r);
-  }
-  __syncthreads();
-}
-
-#ifndef BGV_COOP_CYC_SQR
-#define BGV_COOP_CYC_SQR 0  // measured: batch final exp 2.10 ms against 1.98 with c_mul; both through LDS address-space pointers, 2.07 against 1.68
-#endif
-
 // out = a^x (x < 0) for a in the cyclotomic subgroup
 __device__ void c_pow_x(wfp12* out, const wfp12* a, wfp12* acc, cscratch* s) {
   c_copy(acc, a);
   for (int b = 62; b >= 0; b--) {
-#if BGV_COOP_CYC_SQR
-    c_cyc_sqr(acc, acc, s);
-#else
     c_mul(acc, acc, acc, s);
-#endif
     if ((BLS_X_ABS >> b) & 1ull) c_mul(acc, acc, a, s);
   }
   c_conj(out, acc);
 }
 
-// Final exponentiation with the addition chain of fp12_final_exp; returns
-// (to every thread) whether f^((p^12 - 1)/r) == 1.
-__device__ bool c_final_exp_is_one(const fp12_t& f_in, cscratch* s) {
+// Final exponentiation with the addition chain of fp12_final_exp: out (in
+// LDS, tower form) = f^(3 (p^12 - 1) / r), the cube of the textbook value
+// (the hard-part chain computes m^(3 (p^4 - p^2 + 1) / r); 3 is prime to r,
+// so the value is 1 exactly when the textbook one is).
+__device__ void c_final_exp(fp12_t* out, const fp12_t& f_in, cscratch* s) {
   const uint32_t l = threadIdx.x;
   wfp12 *t0 = &s->t[0], *t1 = &s->t[1], *y0 = &s->t[2], *y1 = &s->t[3], *y2 = &s->t[4], *acc = &s->t[5];
   __shared__ wfp12 fin, y3;
-  __shared__ uint32_t result;
   if (l == 0) {
     // the one Fp12 inversion of the easy part stays on one lane (its Fp
     // inversion is a divstep chain, fp.h)
@@ -331,11 +257,16 @@ __device__ bool c_final_exp_is_one(const fp12_t& f_in, cscratch* s) {
   c_mul(t0, t1, t1, s);
   c_mul(t0, t0, t1, s);  // m^3
   c_mul(&y3, &y3, t0, s);
-  if (l == 0) {
-    fp12_t r;
-    w_to_tower(r, y3);
-    result = fp12_is_one(r) ? 1u : 0u;
-  }
+  if (l == 0) w_to_tower(*out, y3);
+  __syncthreads();
+}
+
+// returns (to every thread) whether f^((p^12 - 1)/r) == 1
+__device__ bool c_final_exp_is_one(const fp12_t& f_in, cscratch* s) {
+  __shared__ fp12_t r;
+  __shared__ uint32_t result;
+  c_final_exp(&r, f_in, s);
+  if (threadIdx.x == 0) result = fp12_is_one(r) ? 1u : 0u;
   __syncthreads();
   return result != 0;
 }

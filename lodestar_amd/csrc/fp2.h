@@ -25,50 +25,8 @@ BGV_HD void fp2_mul3(fp2_t& r, const fp2_t& a) { fp_mul3(r.c0, a.c0); fp_mul3(r.
 BGV_HD void fp2_mul4(fp2_t& r, const fp2_t& a) { fp_mul4(r.c0, a.c0); fp_mul4(r.c1, a.c1); }
 BGV_HD void fp2_mul8(fp2_t& r, const fp2_t& a) { fp_mul8(r.c0, a.c0); fp_mul8(r.c1, a.c1); }
 
-// BGV_FP2_LEAF=1 (device, with BGV_FPMUL_CALL): every Fp2 product is ONE
-// call to a non-inlined leaf running fp2_mul28_lazy (fp.h: 2 reductions for
-// the 3 Karatsuba products).  Its 48 operand dwords exceed the 32 argument
-// VGPRs, so 16 travel through the scratch stack.
-#ifndef BGV_FP2_LEAF
-#define BGV_FP2_LEAF 0
-#endif
-#if defined(__HIPCC__) && BGV_FPMUL_CALL && BGV_FP2_LEAF
-typedef uint32_t fp2_vec_t __attribute__((ext_vector_type(24)));
-static __device__ __noinline__ fp2_vec_t fp2_mul_leaf(fp2_vec_t a, fp2_vec_t b) {
-  fp_t a0, a1, b0, b1, r0, r1;
-#pragma unroll
-  for (int i = 0; i < NL; i++) {
-    a0.l[i] = a[i]; a1.l[i] = a[NL + i];
-    b0.l[i] = b[i]; b1.l[i] = b[NL + i];
-  }
-  fp2_mul28_lazy(r0, r1, a0, a1, b0, b1);
-  fp2_vec_t v;
-#pragma unroll
-  for (int i = 0; i < NL; i++) { v[i] = r0.l[i]; v[NL + i] = r1.l[i]; }
-  return v;
-}
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && BGV_FPMUL_CALL && BGV_FP2_LEAF
-#define BGV_FP2_VIA_LEAF(r, a, b)                                        \
-  do {                                                                   \
-    fp2_vec_t va_, vb_;                                                  \
-    _Pragma("unroll") for (int i_ = 0; i_ < NL; i_++) {                  \
-      va_[i_] = (a).c0.l[i_]; va_[NL + i_] = (a).c1.l[i_];               \
-      vb_[i_] = (b).c0.l[i_]; vb_[NL + i_] = (b).c1.l[i_];               \
-    }                                                                    \
-    const fp2_vec_t vr_ = fp2_mul_leaf(va_, vb_);                        \
-    _Pragma("unroll") for (int i_ = 0; i_ < NL; i_++) {                  \
-      (r).c0.l[i_] = vr_[i_]; (r).c1.l[i_] = vr_[NL + i_];               \
-    }                                                                    \
-  } while (0)
-#endif
-
 // Karatsuba: 3 Fp products
 BGV_NI2 void fp2_mul(fp2_t& r, const fp2_t& a, const fp2_t& b) {
-#ifdef BGV_FP2_VIA_LEAF
-  BGV_FP2_VIA_LEAF(r, a, b);
-  return;
-#endif
   fp_t t0, t1, t2, t3;
   fp_mul(t0, a.c0, b.c0);
   fp_mul(t1, a.c1, b.c1);
@@ -83,10 +41,6 @@ BGV_NI2 void fp2_mul(fp2_t& r, const fp2_t& a, const fp2_t& b) {
 // force-inlined copy for call sites that want the three products scheduled
 // together with their neighbours (Fp6 multiplications, see fp12.h)
 BGV_HD void fp2_mul_inl(fp2_t& r, const fp2_t& a, const fp2_t& b) {
-#ifdef BGV_FP2_VIA_LEAF
-  BGV_FP2_VIA_LEAF(r, a, b);
-  return;
-#endif
   fp_t t0, t1, t2, t3;
   fp_mul(t0, a.c0, b.c0);
   fp_mul(t1, a.c1, b.c1);

@@ -129,41 +129,11 @@ BGV_NI void miller_loop(fp12_t& f, const g1a& P, bool p_inf, const g2a& Q, bool 
 // Two pairs with ONE shared accumulator: f = f_{x,Q1}(P1) * f_{x,Q2}(P2),
 // so the Fp12 squaring of every iteration is paid once for both pairs
 // (the multi-Miller loop of blst's miller_loop_n, at width 2).
-#ifndef BGV_LINE_PAIR
-#define BGV_LINE_PAIR 0  // 1: multiply the two pairs' lines together first (fp12_mul_line2): 12% fewer products, but larger frames (k_miller scratch 7 -> 12 GB) and 19.2 vs 18.9 ms measured
-#endif
 BGV_NI void miller_loop2(fp12_t& f, const g1a& P1, const g2a& Q1, const g1a& P2, const g2a& Q2) {
   g2p_t T1, T2;
   T1.x = Q1.x; T1.y = Q1.y; T1.z = fp2_one();
   T2.x = Q2.x; T2.y = Q2.y; T2.z = fp2_one();
   fp2_t a0, a1, b1;
-#if BGV_LINE_PAIR
-  // f <- f^2 * (l1 l2): the two sparse lines are multiplied together
-  // (6 Fp2 products) and enter f once (17) instead of twice (2 x 13)
-  fp2_t c0, c1, d1;
-  line2_t L;
-  fp12_one(f);
-  for (int b = 62; b >= 0; b--) {
-    if (b != 62) fp12_sqr(f, f);
-    miller_dbl_step(T1, a0, a1, b1, P1.x, P1.y);
-    miller_dbl_step(T2, c0, c1, d1, P2.x, P2.y);
-    if (b == 62) {  // f = 1 * l1, then * l2
-      f.c0.c0 = a0;
-      f.c0.c1 = a1;
-      f.c1.c1 = b1;
-      fp12_mul_line(f, f, c0, c1, d1);
-    } else {
-      line_mul_line(L, a0, a1, b1, c0, c1, d1);
-      fp12_mul_line2(f, f, L);
-    }
-    if ((BLS_X_ABS >> b) & 1ull) {
-      miller_add_step(T1, a0, a1, b1, Q1, P1.x, P1.y);
-      miller_add_step(T2, c0, c1, d1, Q2, P2.x, P2.y);
-      line_mul_line(L, a0, a1, b1, c0, c1, d1);
-      fp12_mul_line2(f, f, L);
-    }
-  }
-#else
   fp12_one(f);
   for (int b = 62; b >= 0; b--) {
     if (b != 62) fp12_sqr(f, f);
@@ -184,7 +154,6 @@ BGV_NI void miller_loop2(fp12_t& f, const g1a& P1, const g2a& Q1, const g1a& P2,
       fp12_mul_line(f, f, a0, a1, b1);
     }
   }
-#endif
   fp12_conj(f, f);  // x < 0
 }
 

@@ -1,13 +1,24 @@
 """Multi-GPU glue for the batch verifier.
 
-Signature sets shard by job across ranks (one process per GPU).  Every rank
-reduces its shard to one Fp12 Miller product (576 B, bgv_partial); the
-partials are all-gathered (RCCL over xGMI on the GPU node, gloo in the CPU
-tests) and multiplied before ONE final exponentiation (bgv_combine_final).
-At 576 B per rank the exchange is latency-bound, so a single all-gather is
-the whole collective; there is no other data-path communication.
+Signature sets shard by job across ranks (one process per GPU; a job is
+never split: its verdict is the AND of its sets).  Every rank reduces its
+shard to one Fp12 Miller product (576 B, bgv_partial); the partials are
+all-gathered (RCCL over xGMI on the GPU node, gloo in the CPU tests) and
+multiplied before ONE final exponentiation (bgv_combine_final).  At 576 B
+per rank the exchange is latency-bound, so a single all-gather is the whole
+collective on the success path.
+
+Failure path (SURVEY §8e "Failure"; the reference always resolves per job,
+multithread/index.ts:356-372, and verifyBlocksSignatures names the first bad
+block, verifyBlocksSignatures.ts:56-59): when the combined check fails, each
+rank runs the final exponentiation of its OWN shard on the intermediates
+bgv_partial left on the device and, only if that fails too, one per job
+(bgv_partial_finish, the worker's per-job retry).  The per-job int32
+verdicts are then all-gathered so every rank holds the whole batch's.
 """
 from __future__ import annotations
+
+import numpy as np
 
 PARTIAL_BYTES = 576
 
@@ -24,6 +35,29 @@ def shard_jobs(job_sizes: list[int], world: int) -> list[list[int]]:
     return [sorted(s) for s in shards]
 
 
+def select_jobs(arrays: dict, jobs: list[int]) -> dict:
+    """The bgv_batch arrays (host, numpy) of a subset of a batch's jobs, with
+    job and pubkey offsets rebased; per-set arrays are sliced, the raw-key
+    table is shared."""
+    jo = np.asarray(arrays["job_offsets"], np.int64)
+    po = np.asarray(arrays["pk_offsets"], np.int64)
+    sets = np.concatenate([np.arange(jo[j], jo[j + 1]) for j in jobs]) if jobs else np.zeros(0, np.int64)
+    sizes = np.array([jo[j + 1] - jo[j] for j in jobs], np.int64)
+    k = po[sets + 1] - po[sets]
+    idx = (np.concatenate([np.arange(po[i], po[i + 1]) for i in sets]) if len(sets) else np.zeros(0, np.int64))
+    out = dict(arrays)
+    out["n_sets"] = int(len(sets))
+    out["n_jobs"] = len(jobs)
+    out["job_offsets"] = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+    out["pk_offsets"] = np.concatenate([[0], np.cumsum(k)]).astype(np.uint32)
+    out["pk_indices"] = np.asarray(arrays["pk_indices"])[idx].astype(np.uint32) if len(idx) else np.zeros(1, np.uint32)
+    for key in ("msgs", "sigs", "sig_len", "scalars"):
+        v = arrays.get(key)
+        if v is not None:
+            out[key] = np.asarray(v)[sets].copy() if len(sets) else np.asarray(v)[:1].copy()
+    return out
+
+
 def allgather_partials(partial: bytes, dist, device=None) -> list[bytes]:
     """All-gather one 576-byte partial per rank; returns them in rank order."""
     import torch
@@ -37,9 +71,37 @@ def allgather_partials(partial: bytes, dist, device=None) -> list[bytes]:
     return [p.cpu().numpy().tobytes() for p in parts]
 
 
-def verify_sharded(dev, arrays: dict, dist, device=None, on_device: bool = False) -> tuple[bool, bool]:
-    """This rank's shard -> partial -> all-gather -> combined final check.
-    Returns (node_batch_valid, this_shard_parsed_ok)."""
-    part, _, ok = dev.partial(arrays, on_device=on_device)
+def verify_sharded(dev, arrays: dict, dist, device=None, on_device: bool = False):
+    """This rank's shard -> partial -> all-gather -> combined final check, and
+    the per-shard localisation when it fails.
+
+    Returns (node_batch_valid, local_job_results): local_job_results[j] is
+    this shard's job j as bgv_verify reports it (1 valid, 0 invalid, -code
+    rejected).  Every rank takes the same branch (the combined verdict is
+    computed from the same all-gathered partials)."""
+    part, _, jobs, _ = dev.partial(arrays, on_device=on_device)
     parts = allgather_partials(part, dist, device)
-    return dev.combine_final(parts), ok
+    if dev.combine_final(parts):
+        return True, np.asarray(jobs, np.int32)
+    return False, np.asarray(dev.partial_finish(), np.int32)
+
+
+def gather_job_results(local: np.ndarray, shards: list[list[int]], n_jobs: int, dist, device=None) -> np.ndarray:
+    """All-gather every rank's per-job verdicts (padded to the largest shard)
+    and place them at their batch job ids: the int32 verdict of every job of
+    the node batch, on every rank."""
+    import torch
+
+    width = max(1, max(len(s) for s in shards))
+    buf = np.zeros(width, np.int32)
+    buf[: len(local)] = local
+    t = torch.from_numpy(buf)
+    if device is not None:
+        t = t.to(device)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    out = np.zeros(n_jobs, np.int32)
+    for r, ids in enumerate(shards):
+        vals = parts[r].cpu().numpy()
+        out[np.asarray(ids, np.int64)] = vals[: len(ids)]
+    return out

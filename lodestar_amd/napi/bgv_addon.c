@@ -9,21 +9,31 @@
  *   pubkeysSet(ctx, first, Uint8Array, format)   bgv_pubkeys_set (pubkeyCache.ts:56-77)
  *   pubkeysCount(ctx) -> number
  *   pubkeysValidate(ctx, Uint8Array) -> Int32Array   bgv_pubkeys_validate (processDeposit.ts:57-66)
- *   verify(ctx, batch) -> Promise<Int32Array>    bgv_verify on the libuv pool (worker.ts:30-106)
- *   verifySync(ctx, batch) -> Int32Array         verifyOnMainThread / BlsSingleThreadVerifier
+ *   verify(ctx, batch) -> Promise<result>        bgv_verify on the libuv pool (worker.ts:30-106)
+ *   verifySync(ctx, batch) -> result             verifyOnMainThread / BlsSingleThreadVerifier
  *
  * batch = {jobOffsets: Uint32Array, pkOffsets: Uint32Array, pkIndices:
  * Uint32Array, msgs: Uint8Array, sigs: Uint8Array (192 B per set), sigLen:
- * Uint32Array, rawPks?: Uint8Array (96 B per key)}.  Per-job results are
- * bgv_job_result values: 1 valid, 0 invalid, -code rejected.  Inputs are
- * pinned by references until the async work completes; the library copies
- * them to HBM and keeps nothing (SURVEY section 8b ownership).  A context is
- * not thread-safe, so calls on one context are serialised by its mutex. */
+ * Uint32Array, rawPks?: Uint8Array (96 B per key)}.
+ * result = {results: Int32Array (bgv_job_result per job: 1 valid, 0 invalid,
+ * -code rejected), batchRetries, batchSigsSuccess, pubkeysAggregated,
+ * deviceMs, workerStartMs, workerEndMs}: the BlsWorkResult fields
+ * (multithread/types.ts:26-38) the pool's metrics are fed from.
+ *
+ * Ownership: the offset arrays are copied when the call
+ * is made and every length is checked against the copies, so a caller that
+ * mutates its typed arrays while the work is queued cannot make the library
+ * read past them; the other arrays are pinned by references until the work
+ * completes (the library copies them to pinned memory and HBM and keeps
+ * nothing).  The context external is referenced by every queued work item,
+ * so it outlives them.  A context is not thread-safe: calls on one context
+ * are serialised by its mutex. */
 #include <node_api.h>
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "bgv.h"
 
@@ -45,7 +55,10 @@ static void ctx_finalize(napi_env env, void* data, void* hint) {
   (void)env;
   (void)hint;
   addon_ctx* c = (addon_ctx*)data;
+  pthread_mutex_lock(&c->mu); /* no work item can hold the context here (each references it), but be exact */
   if (!c->closed) bgv_close(c->ctx);
+  c->closed = 1;
+  pthread_mutex_unlock(&c->mu);
   pthread_mutex_destroy(&c->mu);
   free(c);
 }
@@ -65,7 +78,7 @@ static addon_ctx* get_ctx(napi_env env, napi_value v) {
   }
   addon_ctx* c = (addon_ctx*)p;
   if (c->closed) {
-    napi_throw_error(env, "QUEUE_ABORTED", "bgv context closed");
+    napi_throw_error(env, "QUEUE_ERROR_QUEUE_ABORTED", "QUEUE_ERROR_QUEUE_ABORTED: bgv context closed");
     return NULL;
   }
   return c;
@@ -215,20 +228,33 @@ static const napi_typedarray_type FIELD_T[N_FIELDS] = {napi_uint32_array, napi_u
 typedef struct {
   addon_ctx* c;
   bgv_batch b;
+  uint32_t* job_off; /* copies made at call time (the library reads these) */
+  uint32_t* pk_off;
   int32_t* job_result;
+  bgv_stats stats;
+  double t_start_ms, t_end_ms;
   int status;
   char err[512];
   napi_ref refs[N_FIELDS];
+  napi_ref ctx_ref;
   napi_async_work work;
   napi_deferred deferred;
 } verify_job;
 
-/* reads the batch object into j->b; pins the arrays when pin != 0 */
+static void free_job_arrays(verify_job* j) {
+  free(j->job_off);
+  free(j->pk_off);
+  free(j->job_result);
+  j->job_off = j->pk_off = NULL;
+  j->job_result = NULL;
+}
+
+/* reads the batch object into j->b; copies the offsets; pins the other arrays when pin != 0 */
 static int read_batch(napi_env env, napi_value obj, verify_job* j, int pin) {
   void* p[N_FIELDS] = {0};
   size_t n[N_FIELDS] = {0};
+  napi_value v[N_FIELDS];
   for (int k = 0; k < N_FIELDS; k++) {
-    napi_value v;
     bool has = false;
     napi_has_named_property(env, obj, FIELD[k], &has);
     if (!has) {
@@ -236,12 +262,11 @@ static int read_batch(napi_env env, napi_value obj, verify_job* j, int pin) {
       napi_throw_type_error(env, NULL, "batch field missing");
       return -1;
     }
-    napi_get_named_property(env, obj, FIELD[k], &v);
-    if (typed(env, v, FIELD_T[k], &p[k], &n[k])) {
+    napi_get_named_property(env, obj, FIELD[k], &v[k]);
+    if (typed(env, v[k], FIELD_T[k], &p[k], &n[k])) {
       napi_throw_type_error(env, NULL, "batch field has the wrong typed-array type");
       return -1;
     }
-    if (pin) napi_create_reference(env, v, 1, &j->refs[k]);
   }
   if (n[F_JOB] < 1 || n[F_PKO] < 1) {
     napi_throw_range_error(env, NULL, "jobOffsets / pkOffsets need at least one entry");
@@ -250,12 +275,28 @@ static int read_batch(napi_env env, napi_value obj, verify_job* j, int pin) {
   memset(&j->b, 0, sizeof j->b);
   j->b.n_jobs = (uint32_t)(n[F_JOB] - 1);
   j->b.n_sets = (uint32_t)(n[F_PKO] - 1);
-  if (n[F_MSG] < 32ull * j->b.n_sets || n[F_SIG] < 192ull * j->b.n_sets || n[F_LEN] < j->b.n_sets) {
+  j->job_off = (uint32_t*)malloc(4 * n[F_JOB]);
+  j->pk_off = (uint32_t*)malloc(4 * n[F_PKO]);
+  if (!j->job_off || !j->pk_off) {
+    napi_throw_error(env, NULL, "out of memory");
+    return -1;
+  }
+  memcpy(j->job_off, p[F_JOB], 4 * n[F_JOB]);
+  memcpy(j->pk_off, p[F_PKO], 4 * n[F_PKO]);
+  const uint32_t n_sets = j->b.n_sets;
+  if (n[F_MSG] < 32ull * n_sets || n[F_SIG] < 192ull * n_sets || n[F_LEN] < n_sets) {
     napi_throw_range_error(env, NULL, "msgs / sigs / sigLen shorter than the set count");
     return -1;
   }
-  j->b.job_offsets = (const uint32_t*)p[F_JOB];
-  j->b.pk_offsets = (const uint32_t*)p[F_PKO];
+  if (n[F_PKI] < (size_t)j->pk_off[n_sets]) {
+    napi_throw_range_error(env, NULL, "pkIndices shorter than pkOffsets[n_sets]");
+    return -1;
+  }
+  if (pin)
+    for (int k = 0; k < N_FIELDS; k++)
+      if (p[k] && k != F_JOB && k != F_PKO) napi_create_reference(env, v[k], 1, &j->refs[k]);
+  j->b.job_offsets = j->job_off;
+  j->b.pk_offsets = j->pk_off;
   j->b.pk_indices = (const uint32_t*)p[F_PKI];
   j->b.msgs = (const uint8_t*)p[F_MSG];
   j->b.sigs = (const uint8_t*)p[F_SIG];
@@ -267,16 +308,46 @@ static int read_batch(napi_env env, napi_value obj, verify_job* j, int pin) {
   return 0;
 }
 
+static double now_ms(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double)t.tv_sec * 1e3 + (double)t.tv_nsec * 1e-6;
+}
+
 static void run_verify(verify_job* j) {
   pthread_mutex_lock(&j->c->mu);
+  j->t_start_ms = now_ms();
   if (j->c->closed) {
     j->status = BGV_E_INVALID_ARG;
-    snprintf(j->err, sizeof j->err, "QUEUE_ABORTED");
+    snprintf(j->err, sizeof j->err, "QUEUE_ERROR_QUEUE_ABORTED");
   } else {
-    j->status = bgv_verify(j->c->ctx, &j->b, j->job_result, NULL, NULL);
+    j->status = bgv_verify(j->c->ctx, &j->b, j->job_result, NULL, &j->stats);
     if (j->status != BGV_OK) snprintf(j->err, sizeof j->err, "bgv error %d: %s", j->status, bgv_last_error());
   }
+  j->t_end_ms = now_ms();
   pthread_mutex_unlock(&j->c->mu);
+}
+
+/* {results, batchRetries, batchSigsSuccess, pubkeysAggregated, deviceMs, workerStartMs, workerEndMs} */
+static napi_value result_object(napi_env env, const verify_job* j) {
+  napi_value o, v;
+  if (napi_create_object(env, &o) != napi_ok) return NULL;
+  v = new_int32_array(env, j->job_result, j->b.n_jobs);
+  if (!v) return NULL;
+  napi_set_named_property(env, o, "results", v);
+  napi_create_uint32(env, j->stats.batch_retries, &v);
+  napi_set_named_property(env, o, "batchRetries", v);
+  napi_create_uint32(env, j->stats.batch_sigs_success, &v);
+  napi_set_named_property(env, o, "batchSigsSuccess", v);
+  napi_create_double(env, (double)j->stats.pubkeys_aggregated, &v);
+  napi_set_named_property(env, o, "pubkeysAggregated", v);
+  napi_create_double(env, (double)j->stats.total_ms, &v);
+  napi_set_named_property(env, o, "deviceMs", v);
+  napi_create_double(env, j->t_start_ms, &v);
+  napi_set_named_property(env, o, "workerStartMs", v);
+  napi_create_double(env, j->t_end_ms, &v);
+  napi_set_named_property(env, o, "workerEndMs", v);
+  return o;
 }
 
 static void exec_verify(napi_env env, void* data) { /* libuv worker thread */
@@ -296,13 +367,13 @@ static void done_verify(napi_env env, napi_status st, void* data) { /* main thre
     napi_create_error(env, NULL, msg, &err);
     napi_reject_deferred(env, j->deferred, err);
   } else {
-    napi_value arr = new_int32_array(env, j->job_result, j->b.n_jobs);
-    napi_resolve_deferred(env, j->deferred, arr);
+    napi_resolve_deferred(env, j->deferred, result_object(env, j));
   }
   for (int k = 0; k < N_FIELDS; k++)
     if (j->refs[k]) napi_delete_reference(env, j->refs[k]); /* unpin the inputs */
+  if (j->ctx_ref) napi_delete_reference(env, j->ctx_ref);
   napi_delete_async_work(env, j->work);
-  free(j->job_result);
+  free_job_arrays(j);
   free(j);
 }
 
@@ -317,9 +388,11 @@ static napi_value Verify(napi_env env, napi_callback_info info) {
   if (read_batch(env, a[1], j, 1)) {
     for (int k = 0; k < N_FIELDS; k++)
       if (j->refs[k]) napi_delete_reference(env, j->refs[k]);
+    free_job_arrays(j);
     free(j);
     return NULL;
   }
+  napi_create_reference(env, a[0], 1, &j->ctx_ref); /* the context outlives its queued work */
   j->job_result = (int32_t*)calloc(j->b.n_jobs ? j->b.n_jobs : 1, 4);
   napi_value promise, name;
   NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
@@ -338,13 +411,16 @@ static napi_value VerifySync(napi_env env, napi_callback_info info) {
   verify_job j;
   memset(&j, 0, sizeof j);
   j.c = c;
-  if (read_batch(env, a[1], &j, 0)) return NULL;
+  if (read_batch(env, a[1], &j, 0)) {
+    free_job_arrays(&j);
+    return NULL;
+  }
   j.job_result = (int32_t*)calloc(j.b.n_jobs ? j.b.n_jobs : 1, 4);
   run_verify(&j);
   napi_value r = NULL;
   if (j.status != BGV_OK) napi_throw_error(env, NULL, j.err);
-  else r = new_int32_array(env, j.job_result, j.b.n_jobs);
-  free(j.job_result);
+  else r = result_object(env, &j);
+  free_job_arrays(&j);
   return r;
 }
 

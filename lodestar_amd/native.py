@@ -23,6 +23,9 @@ BGV_E_HIP = -2
 BGV_E_NO_DEVICE = -3
 BGV_E_TABLE_RANGE = -4
 BGV_E_EMPTY_SET = -5
+BGV_E_BAD_PUBKEY = -6
+BGV_E_STATE = -7
+ABI_VERSION = 2
 
 SET_CODE_NAMES = {
     0: "BLST_SUCCESS",
@@ -40,12 +43,13 @@ SET_CODE_NAMES = {
 
 PK_COMPRESSED_48 = 0
 PK_UNCOMPRESSED_96 = 1
-N_STAGES = 12
+N_STAGES = 16
 
 EXPORTS = [
     "bgv_abi_version", "bgv_set_code_name", "bgv_stage_name", "bgv_last_error", "bgv_open", "bgv_close",
-    "bgv_pubkeys_set", "bgv_pubkeys_count", "bgv_pubkeys_get", "bgv_pubkeys_validate", "bgv_verify", "bgv_partial",
-    "bgv_combine_final", "bgv_gen_keys", "bgv_gen_sign", "bgv_bench_fpmul", "bgv_bench_mad",
+    "bgv_pubkeys_set", "bgv_pubkeys_count", "bgv_pubkeys_get", "bgv_pubkeys_validate", "bgv_verify", "bgv_last_stats",
+    "bgv_partial", "bgv_partial_finish", "bgv_combine_final", "bgv_debug_stages", "bgv_gen_keys", "bgv_gen_sign", "bgv_bench_fpmul",
+    "bgv_bench_mad",
 ]
 
 
@@ -96,6 +100,12 @@ class BgvStats(ctypes.Structure):
         }
 
 
+class BgvDebug(ctypes.Structure):
+    """bgv_debug (include/bgv.h): host buffers for bgv_debug_stages."""
+    _fields_ = [(k, ctypes.c_void_p) for k in
+                ("sig_aff", "h_aff", "pk_agg", "rpk_aff", "s_aff", "pair_fe", "job_fe", "batch_fe")]
+
+
 _lib = None
 _lib_lock = threading.Lock()
 
@@ -123,7 +133,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
             "bgv_pubkeys_get": ([P, u32, u32, P], ctypes.c_int),
             "bgv_pubkeys_validate": ([P, P, u32, P], ctypes.c_int),
             "bgv_verify": ([P, ctypes.POINTER(BgvBatch), P, P, ctypes.POINTER(BgvStats)], ctypes.c_int),
-            "bgv_partial": ([P, ctypes.POINTER(BgvBatch), P, P, ctypes.POINTER(i32)], ctypes.c_int),
+            "bgv_partial": ([P, ctypes.POINTER(BgvBatch), P, P, P, ctypes.POINTER(i32)], ctypes.c_int),
+            "bgv_partial_finish": ([P, P, ctypes.POINTER(BgvStats)], ctypes.c_int),
+            "bgv_last_stats": ([P, ctypes.POINTER(BgvStats)], ctypes.c_int),
+            "bgv_debug_stages": ([P, ctypes.POINTER(BgvBatch), P, P, ctypes.POINTER(BgvDebug)], ctypes.c_int),
             "bgv_combine_final": ([P, P, u32, ctypes.POINTER(i32)], ctypes.c_int),
             "bgv_gen_keys": ([P, u32, u32, u64], ctypes.c_int),
             "bgv_gen_sign": ([P, ctypes.POINTER(BgvBatch), P], ctypes.c_int),
@@ -134,6 +147,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = res
+        if lib.bgv_abi_version() != ABI_VERSION:
+            raise BgvNativeError(BGV_E_INVALID_ARG, f"{path}: ABI {lib.bgv_abi_version()}, expected {ABI_VERSION} (rebuild)")
         _lib = lib
         return lib
 
@@ -234,12 +249,43 @@ class Device:
         return jr[: b.n_jobs], (sc[: b.n_sets] if sc is not None else None)
 
     def partial(self, arrays: dict, on_device: bool = False):
+        """bgv_partial: (miller576 bytes, set codes, provisional job results
+        (-code rejected / 1 pending the combined check), no-job-rejected)."""
         b = self.make_batch(arrays, on_device)
         out = np.zeros(576, dtype=np.uint8)
         sc = np.zeros(max(b.n_sets, 1), dtype=np.int32)
+        jr = np.zeros(max(b.n_jobs, 1), dtype=np.int32)
         ok = ctypes.c_int32()
-        self._check(self.lib.bgv_partial(self.h, ctypes.byref(b), out.ctypes.data, sc.ctypes.data, ctypes.byref(ok)))
-        return out.tobytes(), sc[: b.n_sets], bool(ok.value)
+        self._check(self.lib.bgv_partial(self.h, ctypes.byref(b), out.ctypes.data, sc.ctypes.data, jr.ctypes.data,
+                                         ctypes.byref(ok)))
+        self._partial_jobs = b.n_jobs
+        self._check(self.lib.bgv_last_stats(self.h, ctypes.byref(self.last_stats)))
+        return out.tobytes(), sc[: b.n_sets], jr[: b.n_jobs], bool(ok.value)
+
+    def partial_finish(self) -> np.ndarray:
+        """bgv_partial_finish: per-job verdicts of the shard left by partial()."""
+        n = getattr(self, "_partial_jobs", 0)
+        jr = np.zeros(max(n, 1), dtype=np.int32)
+        self._check(self.lib.bgv_partial_finish(self.h, jr.ctypes.data, ctypes.byref(self.last_stats)))
+        return jr[:n]
+
+    def debug_stages(self, arrays: dict, on_device: bool = False) -> dict:
+        """bgv_debug_stages (test only): per-stage canonical values as numpy arrays."""
+        b = self.make_batch(arrays, on_device)
+        n, J = b.n_sets, b.n_jobs
+        bufs = {"sig_aff": np.zeros((max(n, 1), 192), np.uint8), "h_aff": np.zeros((max(n, 1), 192), np.uint8),
+                "pk_agg": np.zeros((max(n, 1), 96), np.uint8), "rpk_aff": np.zeros((max(n, 1), 96), np.uint8),
+                "s_aff": np.zeros((max(J, 1), 192), np.uint8), "pair_fe": np.zeros((max(n + J, 1), 576), np.uint8),
+                "job_fe": np.zeros((max(J, 1), 576), np.uint8), "batch_fe": np.zeros(576, np.uint8)}
+        dbg = BgvDebug(**{k: v.ctypes.data for k, v in bufs.items()})
+        jr = np.zeros(max(J, 1), dtype=np.int32)
+        sc = np.zeros(max(n, 1), dtype=np.int32)
+        self._check(self.lib.bgv_debug_stages(self.h, ctypes.byref(b), jr.ctypes.data, sc.ctypes.data, ctypes.byref(dbg)))
+        out = {k: (v[: n] if k in ("sig_aff", "h_aff", "pk_agg", "rpk_aff") else v[: J] if k in ("s_aff", "job_fe")
+                   else v[: n + J] if k == "pair_fe" else v) for k, v in bufs.items()}
+        out["job_result"] = jr[:J]
+        out["set_code"] = sc[:n]
+        return out
 
     def combine_final(self, partials: list[bytes]) -> bool:
         buf = np.frombuffer(b"".join(partials), dtype=np.uint8) if partials else np.zeros(1, np.uint8)

@@ -153,21 +153,34 @@ class PubkeyTable:
         return self.devices[0].pubkeys_count()
 
     def sync_pubkeys(self, pubkeys48: list[bytes]):
-        """Append every validator pubkey not yet in the table (compressed)."""
+        """Append every validator pubkey not yet in the table (compressed).
+        A key that does not deserialize throws like PublicKey.fromBytes and
+        leaves the table unchanged."""
+        if len(self.pubkey2index) != len(self):  # pubkeyCache.ts:61-63
+            raise BlsError(f"Pubkey indices have fallen out of sync: {len(self.pubkey2index)} != {len(self)}")
         start = len(self)
         new = pubkeys48[start:]
         if not new:
             return
         blob = b"".join(new)
-        for d in self.devices:
-            d.pubkeys_set(start, blob, native.PK_COMPRESSED_48)
+        self._set(start, blob)
         for i, pk in enumerate(new):
             self.pubkey2index[bytes(pk)] = start + i
 
     def add_pubkey(self, index: int, pubkey48: bytes):
-        for d in self.devices:
-            d.pubkeys_set(index, pubkey48, native.PK_COMPRESSED_48)
+        """epochContext.ts:701-704.  The device table is append-only: index
+        may rewrite a row or append the next one, not leave a gap."""
+        self._set(index, pubkey48)
         self.pubkey2index[bytes(pubkey48)] = index
+
+    def _set(self, first: int, blob: bytes):
+        for d in self.devices:
+            try:
+                d.pubkeys_set(first, blob, native.PK_COMPRESSED_48)
+            except native.BgvNativeError as e:
+                if e.status == native.BGV_E_BAD_PUBKEY:
+                    raise BlsError(str(e).split(": ", 1)[-1]) from e
+                raise
 
     def __getitem__(self, index: int) -> PublicKey:
         return PublicKey(index=index)
@@ -231,6 +244,27 @@ def _decompress_raw48(b: bytes) -> bytes:
     raise BlsError("raw compressed pubkeys must be added to the table (PubkeyTable.add_pubkey)")
 
 
+def check_sets(sets: list[ISignatureSet]) -> None:
+    """Caller-side checks of one verifySignatureSets call: PublicKey.aggregate
+    throws EMPTY_AGGREGATE_ARRAY (chain/bls/utils.ts:11); a raw key must be a
+    96-byte uncompressed point (compressed keys live in the table); a signing
+    root is 32 bytes.  Pubkey indices past the table are reported per set by
+    the device (BGV_INDEX_RANGE rejects only that job)."""
+    for s in sets:
+        pks = [s.pubkey] if s.type == SignatureSetType.single else s.pubkeys
+        if s.type == SignatureSetType.aggregate and len(pks) == 0:
+            raise BlsError("EMPTY_AGGREGATE_ARRAY")
+        for pk in pks:
+            if pk is None:
+                raise BlsError("EMPTY_AGGREGATE_ARRAY")
+            if pk.index is None and len(pk.raw) != 96:
+                _decompress_raw48(pk.raw)
+            if pk.index is not None and not (0 <= pk.index < 0x80000000):
+                raise BlsError(f"pubkey index {pk.index} out of range")
+        if len(s.signingRoot) != 32:
+            raise BlsError("signingRoot must be 32 bytes")
+
+
 # ----------------------------------------------------------------- verifier
 @dataclass
 class _Job:
@@ -270,9 +304,10 @@ class BlsGpuVerifier:
     async def verify_signature_sets(self, sets: list[ISignatureSet], opts: VerifySignatureOpts | None = None) -> bool:
         opts = opts or VerifySignatureOpts()
         self.metrics["aggregated_pubkeys_total"] += get_aggregated_pubkeys_count(sets)
-        for s in sets:  # PublicKey.aggregate throws on the main thread (utils.ts:11)
-            if s.type == SignatureSetType.aggregate and len(s.pubkeys) == 0:
-                raise BlsError("EMPTY_AGGREGATE_ARRAY")
+        # the checks the reference makes on the caller's side before queueing
+        # (getAggregatedPubkey, utils.ts:5-16), so a bad call cannot fail a
+        # device batch it shares with other callers
+        check_sets(sets)
         if opts.verifyOnMainThread:
             # unbuffered, high priority: one device batch right now
             res = await asyncio.get_running_loop().run_in_executor(self._exec, self._run_device_batch, [sets])
@@ -304,6 +339,7 @@ class BlsGpuVerifier:
     def verify_signature_sets_maybe_batch(self, sets: list[ISignatureSet]) -> bool:
         """maybeBatch.ts:16-38 for one job, synchronously (BlsSingleThreadVerifier
         path, singleThread.ts:14-35)."""
+        check_sets(sets)
         r = self._run_device_batch([sets])[0]
         if isinstance(r, Exception):
             raise r
@@ -418,17 +454,17 @@ class BlsGpuVerifier:
             sub = [jobs[k] for k in ids]
             try:
                 arrays = encode_jobs(sub, self._scalars(sum(len(j) for j in sub)))
-            except BlsError as e:
+                with self._dev_locks[d]:
+                    t0 = time.perf_counter()
+                    jr, _ = self.devices[d].verify(arrays, want_set_codes=False)
+                    st = self.devices[d].last_stats
+                    self.metrics["batch_retries"] += int(st.batch_retries)
+                    self.metrics["batch_sigs_success"] += int(st.batch_sigs_success)
+                    self.metrics["device_time_s"] += time.perf_counter() - t0
+            except Exception as e:  # noqa: BLE001 -- a device error rejects this shard's jobs (index.ts:386-393)
                 for k in ids:
                     out[k] = e
                 return
-            with self._dev_locks[d]:
-                t0 = time.perf_counter()
-                jr, _ = self.devices[d].verify(arrays, want_set_codes=False)
-                st = self.devices[d].last_stats
-                self.metrics["batch_retries"] += int(st.batch_retries)
-                self.metrics["batch_sigs_success"] += int(st.batch_sigs_success)
-                self.metrics["device_time_s"] += time.perf_counter() - t0
             for k, r in zip(ids, jr.tolist()):
                 out[k] = True if r == 1 else False if r == 0 else error_for_code(-r)
 
@@ -479,9 +515,7 @@ async def verify_blocks_signatures(bls: "BlsGpuVerifier", blocks_sets: list[list
     jobs = []
     owner = []
     for b, sets in enumerate(blocks_sets):
-        for s in sets:
-            if s.type == SignatureSetType.aggregate and len(s.pubkeys) == 0:
-                raise BlsError("EMPTY_AGGREGATE_ARRAY")
+        check_sets(sets)
         for chunk in chunkify_maximize_chunk_size(sets, MAX_SIGNATURE_SETS_PER_JOB):
             jobs.append(chunk)
             owner.append(b)

@@ -488,13 +488,19 @@ def g2_decompress(b: bytes):
 
 
 def g2_deserialize(b: bytes):
-    """192-byte uncompressed G2 -> (code, point).  blst POINTonE2_Deserialize_Z."""
+    """192-byte uncompressed G2 -> (code, point).  blst POINTonE2_Deserialize_Z
+    as @chainsafe/blst reaches it through P2_Affine(bytes, len): a 192-byte
+    input must not carry the compression flag (len != (in[0] & 0x80 ? 96 :
+    192) is BAD_ENCODING), the infinity flag needs every other bit zero, and
+    the sign flag (0x20) on an uncompressed encoding is BAD_ENCODING."""
     b0 = b[0]
     if b0 & 0x80:
         return BLST_BAD_ENCODING, None
     if b0 & 0x40:
         if (b0 & 0x3F) == 0 and not any(b[1:192]):
             return BLST_SUCCESS, None
+        return BLST_BAD_ENCODING, None
+    if b0 & 0x20:
         return BLST_BAD_ENCODING, None
     x1 = _be(bytes([b0 & 0x1F]) + b[1:48])
     x0 = _be(b[48:96])

@@ -599,6 +599,7 @@ static int g2_decode(g2a* out, const uint8_t* b, int len) {
     out->inf = 1;
     return OK;
   }
+  if (b0 & 0x20) return BAD_ENCODING; /* a sign bit only exists on compressed encodings */
   uint8_t t[48];
   memcpy(t, b, 48);
   t[0] &= 0x1f;

@@ -8,7 +8,7 @@ const assert = require("assert");
 const fs = require("fs");
 const path = require("path");
 
-const {addon, BlsGpuVerifier} = require(path.join(__dirname, "..", "..", "lodestar_amd", "napi"));
+const {addon, BlsGpuVerifier, QueueError} = require(path.join(__dirname, "..", "..", "lodestar_amd", "napi"));
 const golden = path.join(__dirname, "..", "golden");
 const hex = (s) => Uint8Array.from(Buffer.from(s.replace(/^0x/, ""), "hex"));
 
@@ -53,17 +53,29 @@ async function main() {
 
   const verifier = new BlsGpuVerifier({device: 0});
   verifier.syncPubkeys(0, pk48);
-  assert.strictEqual(addon.pubkeysCount(verifier.ctx), interop.length);
+  const extra = new Uint8Array(96 * v.extra_table.length);
+  v.extra_table.forEach((p, k) => extra.set(hex(p), 96 * k));
+  addon.pubkeysSet(verifier.ctx, v.extra_table_base, extra, 1);
+  assert.strictEqual(addon.pubkeysCount(verifier.ctx), interop.length + v.extra_table.length);
   assert.deepStrictEqual(Array.from(addon.pubkeysValidate(verifier.ctx, pk48.slice(0, 48 * 4))), [0, 0, 0, 0]);
+  // a gap in the table and an undecodable key are refused
+  assert.throws(() => addon.pubkeysSet(verifier.ctx, 5000, pk48.slice(0, 48), 0), /bgv error -4/);
+  const badKey = pk48.slice(0, 48);
+  badKey[0] &= 0x7f;
+  assert.throws(() => addon.pubkeysSet(verifier.ctx, 102, badKey, 0), /BLST_BAD_ENCODING/);
 
   // 1. golden batch, async (libuv pool) and sync paths
   const {batch, expected} = goldenBatch(v);
   const got = await addon.verify(verifier.ctx, batch);
-  assert.deepStrictEqual(Array.from(got), expected, "addon.verify vs golden");
-  assert.deepStrictEqual(Array.from(addon.verifySync(verifier.ctx, batch)), expected, "addon.verifySync vs golden");
+  assert.deepStrictEqual(Array.from(got.results), expected, "addon.verify vs golden");
+  assert.strictEqual(got.batchRetries, 1);
+  assert.ok(got.deviceMs > 0 && got.workerEndMs >= got.workerStartMs);
+  assert.deepStrictEqual(Array.from(addon.verifySync(verifier.ctx, batch).results), expected, "addon.verifySync vs golden");
   // several in flight at once on one context (serialised by the addon)
   const many = await Promise.all([0, 1, 2, 3].map(() => addon.verify(verifier.ctx, batch)));
-  for (const r of many) assert.deepStrictEqual(Array.from(r), expected);
+  for (const r of many) assert.deepStrictEqual(Array.from(r.results), expected);
+  // pkIndices shorter than pkOffsets[n] is refused before any work is queued
+  assert.throws(() => addon.verify(verifier.ctx, {...batch, pkIndices: batch.pkIndices.slice(0, 3)}), /pkIndices shorter/);
 
   // 2. IBlsVerifier semantics (multithread.test.ts:8-104)
   const sets = v.jobs[0].sets.map((s) => ({
@@ -86,9 +98,46 @@ async function main() {
   }));
   assert.strictEqual(await verifier.verifySignatureSets(agg), v.jobs[1].expected === 1);
 
+  // 3. pool scheduling (multithread/index.ts:143-149, 255-431)
+  const m = verifier.metrics;
+  assert.strictEqual(verifier.canAcceptWork(), true);
+  // two batchable calls inside 100 ms are buffered and run as ONE device batch of two jobs
+  let groups = m.lodestar_bls_thread_pool_job_groups_started_total;
+  let jobsStarted = m.lodestar_bls_thread_pool_jobs_started_total;
+  let waits = m.lodestar_bls_thread_pool_queue_job_wait_time_seconds;
+  let w0 = {...waits};
+  const t0 = Date.now();
+  const [b1, b2] = await Promise.all([verifier.verifySignatureSets(sets, {batchable: true}), verifier.verifySignatureSets(sets, {batchable: true})]);
+  assert.ok(b1 && b2);
+  assert.strictEqual(m.lodestar_bls_thread_pool_job_groups_started_total - groups, 1);
+  assert.strictEqual(m.lodestar_bls_thread_pool_jobs_started_total - jobsStarted, 2);
+  assert.ok(Date.now() - t0 >= 95, "buffered for the 100 ms window");
+  assert.ok((waits.sum - w0.sum) / (waits.count - w0.count) >= 0.09, "queue wait covers the buffer window");
+  // more than 32 buffered sigs flush at once
+  const many33 = [];
+  for (let k = 0; k < 11; k++) many33.push(...sets);
+  groups = m.lodestar_bls_thread_pool_job_groups_started_total;
+  w0 = {...waits};
+  assert.strictEqual(await verifier.verifySignatureSets(many33, {batchable: true}), true);
+  assert.strictEqual(m.lodestar_bls_thread_pool_job_groups_started_total - groups, 1);
+  assert.ok((waits.sum - w0.sum) / (waits.count - w0.count) < 0.09, "a > 32-sig buffer does not wait for the timer");
+  // metrics: retries on a failing batch, sets counted, aggregated keys
+  const retries = m.lodestar_bls_thread_pool_batch_retries_total;
+  assert.strictEqual(await verifier.verifySignatureSets(wrongMsg), false);
+  assert.strictEqual(m.lodestar_bls_thread_pool_batch_retries_total - retries, 1);
+  assert.ok(m.lodestar_bls_thread_pool_batch_sigs_success_total > 0);
+  assert.ok(m.lodestar_bls_thread_pool_success_jobs_signature_sets_count > 0);
+  assert.ok(m.lodestar_bls_thread_pool_error_jobs_signature_sets_count >= 1);
+  assert.strictEqual(m.lodestar_bls_aggregated_pubkeys_total, 5 + 1);  // the k=5 aggregate (+ the empty one)
+  assert.strictEqual(verifier.metricsSnapshot().lodestar_bls_thread_pool_queue_length, 0);
+
+  // 4. close(): buffered and queued jobs reject with QueueError QUEUE_ABORTED
+  const pending = verifier.verifySignatureSets(sets, {batchable: true});
   await verifier.close();
-  await assert.rejects(verifier.verifySignatureSets(sets), /QUEUE_ABORTED/);
-  console.log("addon golden test OK:", Array.from(got).join(","));
+  await assert.rejects(pending, (e) => e instanceof QueueError && e.type.code === "QUEUE_ERROR_QUEUE_ABORTED");
+  await assert.rejects(verifier.verifySignatureSets(sets), /QUEUE_ERROR_QUEUE_ABORTED/);
+  assert.strictEqual(verifier.canAcceptWork(), false);
+  console.log("addon golden test OK:", Array.from(got.results).join(","));
 }
 
 main().catch((e) => {

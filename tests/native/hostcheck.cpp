@@ -71,17 +71,6 @@ int hc_lazy_mul_canonical(uint64_t seed, int n) {
     fp_sqr28(s3, ap);
     for (int i = 0; i < NL; i++) if (s1.l[i] != s2.l[i] || s1.l[i] != s3.l[i]) { bad++; break; }
     if (!fp_plain_lt_p(s3)) bad++;
-    // Fp2 product with lazy reduction against the three-product Karatsuba
-    {
-      fp2_t x, y, z1;
-      x.c0 = a; x.c1 = b; y.c0 = b; y.c1 = a;
-      if (it & 1) { y.c0 = r2; }
-      if (it % 7 == 3) { fp_set_zero(x.c1); }
-      fp2_mul(z1, x, y);
-      fp_t q0, q1;
-      fp2_mul28_lazy(q0, q1, x.c0, x.c1, y.c0, y.c1);
-      for (int i = 0; i < NL; i++) if (q0.l[i] != z1.c0.l[i] || q1.l[i] != z1.c1.l[i]) { bad++; break; }
-    }
   }
   return bad;
 }

@@ -40,12 +40,15 @@ def test_struct_layout_matches_ctypes(tmp_path):
     c = tmp_path / "layout.c"
     fields_b = [f for f, _ in native.BgvBatch._fields_]
     fields_s = [f for f, _ in native.BgvStats._fields_]
+    fields_d = [f for f, _ in native.BgvDebug._fields_]
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "bgv.h"', "int main(void){"]
-    lines.append('printf("%zu %zu\\n", sizeof(bgv_batch), sizeof(bgv_stats));')
+    lines.append('printf("%zu %zu %zu\\n", sizeof(bgv_batch), sizeof(bgv_stats), sizeof(bgv_debug));')
     for f in fields_b:
         lines.append(f'printf("%zu\\n", offsetof(bgv_batch, {f}));')
     for f in fields_s:
         lines.append(f'printf("%zu\\n", offsetof(bgv_stats, {f}));')
+    for f in fields_d:
+        lines.append(f'printf("%zu\\n", offsetof(bgv_debug, {f}));')
     lines.append("return 0;}")
     c.write_text("\n".join(lines))
     exe = tmp_path / "layout"
@@ -53,17 +56,21 @@ def test_struct_layout_matches_ctypes(tmp_path):
     vals = subprocess.check_output([str(exe)]).decode().split()
     assert int(vals[0]) == ctypes.sizeof(native.BgvBatch)
     assert int(vals[1]) == ctypes.sizeof(native.BgvStats)
-    offs = [int(v) for v in vals[2:]]
-    assert offs[: len(fields_b)] == [getattr(native.BgvBatch, f).offset for f in fields_b]
-    assert offs[len(fields_b):] == [getattr(native.BgvStats, f).offset for f in fields_s]
+    assert int(vals[2]) == ctypes.sizeof(native.BgvDebug)
+    offs = [int(v) for v in vals[3:]]
+    nb, ns = len(fields_b), len(fields_s)
+    assert offs[:nb] == [getattr(native.BgvBatch, f).offset for f in fields_b]
+    assert offs[nb:nb + ns] == [getattr(native.BgvStats, f).offset for f in fields_s]
+    assert offs[nb + ns:] == [getattr(native.BgvDebug, f).offset for f in fields_d]
 
 
 def test_metadata_and_no_silent_fallback(lib):
     from lodestar_amd import native
-    assert lib.bgv_abi_version() == 1
+    assert lib.bgv_abi_version() == native.ABI_VERSION == 2
     assert lib.bgv_set_code_name(8) == b"BLST_INVALID_SIZE"
     assert lib.bgv_set_code_name(3) == b"BLST_POINT_NOT_IN_GROUP"
-    assert lib.bgv_stage_name(5) == b"miller_loop"
+    assert lib.bgv_stage_name(6) == b"miller_loop"
+    assert lib.bgv_stage_name(2) == b"pk_gather"
     try:
         import torch
         has_gpu = torch.cuda.is_available()

@@ -20,8 +20,11 @@ def C():
 
 
 def test_sk_to_pk_matches_interop_kat(C):
+    """all 100 keys of the reference's test-cache/interop-pubkeys.json =
+    compress(sk_i G1), sk_i from interop.ts:19-23"""
     pks = json.load(open(os.path.join(G.GOLDEN, "interop-pubkeys.json")))
-    for i in (0, 1, 2, 50, 99):
+    assert len(pks) == 100
+    for i in range(100):
         sk = B.interop_secret_key(i)
         pt = B.g1_decompress(bytes.fromhex(pks[i][2:]))[1]
         assert C.sk_to_pk(sk) == B.g1_serialize(pt)
@@ -43,17 +46,27 @@ def test_golden_jobs(C):
     v = G.batch_vectors()
     pks48 = G.interop_pubkeys48()
     raw = [bytes.fromhex(p) for p in v["raw_pubkeys"]]
+    base, extra = v["extra_table_base"], [bytes.fromhex(p) for p in v["extra_table"]]
+
+    def row(i):
+        return extra[i - base] if i >= base else B.g1_serialize(B.g1_decompress(pks48[48 * i : 48 * i + 48])[1])
+
+    checked = 0
     for jid, job in enumerate(v["jobs"]):
         pks, msgs, sigs = [], [], []
+        if any(s["raw"] is None and max(s["pk"]) >= base + len(extra) for s in job["sets"]):
+            assert job["expected"] == -9  # index past the table: rejected by construction
+            continue
         for s in job["sets"]:
             if s["raw"] is not None:
                 pks.append(raw[s["raw"]])
             else:
-                pts = [B.g1_serialize(B.g1_decompress(pks48[48 * i : 48 * i + 48])[1]) for i in s["pk"]]
-                pks.append(C.aggregate(pts))
+                pks.append(C.aggregate([row(i) for i in s["pk"]]))
             msgs.append(bytes.fromhex(s["msg"]))
             sigs.append(bytes.fromhex(s["sig"]))
         assert C.verify_job(pks, msgs, sigs) == job["expected"], jid
+        checked += 1
+    assert checked == len(v["jobs"]) - 1
 
 
 def test_aggregate_matches_python(C):

@@ -1,9 +1,17 @@
-"""world_size-2 gloo run of the multi-GPU exchange (lodestar_amd/dist.py) on
-CPU: each rank's 576-byte Miller partial reaches every rank in rank order,
-and the shard assignment covers every job exactly once."""
+"""world_size-2 gloo runs of the multi-GPU path (lodestar_amd/dist.py) on CPU:
+the 576-byte Miller partials reach every rank in rank order, the shard
+assignment covers every job exactly once, and the per-job verdicts of a node
+batch are reassembled on every rank, both when the combined check passes and
+when one shard holds a bad job (SURVEY §8e "Failure": the shards localise
+with their own final exponentiations, then the verdicts are all-gathered).
+
+The device is a stand-in with the bgv_partial / bgv_combine_final /
+bgv_partial_finish contract (include/bgv.h); the arithmetic behind it is
+covered by the GPU tests."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
@@ -16,32 +24,90 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+class FakeShardDevice:
+    """bgv_partial contract over known per-job outcomes: the partial encodes
+    whether the shard's non-rejected jobs all verify; combine_final is the AND
+    over the gathered partials; partial_finish reports the per-job outcomes."""
+
+    def __init__(self, truth):
+        self.truth = np.asarray(truth, np.int32)
+        self.finished = 0
+
+    def partial(self, arrays, on_device=False):
+        t = self.truth[np.asarray(arrays["jobs"], np.int64)]
+        ok_pairing = bool(((t == 1) | (t < 0)).all())
+        part = bytes([1 if ok_pairing else 0]) * 576
+        prov = np.where(t < 0, t, 1).astype(np.int32)
+        self._t = t
+        return part, np.zeros(0, np.int32), prov, bool((t >= 0).all())
+
+    def combine_final(self, parts):
+        return all(p[0] == 1 for p in parts)
+
+    def partial_finish(self):
+        self.finished += 1
+        return self._t.copy()
+
+
+def _worker(rank, world, port, q, truth):
     import torch.distributed as dist
-    from lodestar_amd.dist import allgather_partials, shard_jobs
+    from lodestar_amd.dist import allgather_partials, gather_job_results, shard_jobs, verify_sharded
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     part = bytes([rank + 1]) * 576
     parts = allgather_partials(part, dist)
-    shards = shard_jobs([98] * 10, world)
-    q.put((rank, [p[0] for p in parts], [len(p) for p in parts], shards[rank]))
+    shards = shard_jobs([98] * 9 + [40], world)
+    out = {"firsts": [p[0] for p in parts], "lens": [len(p) for p in parts], "shard": shards[rank]}
+    for name, t in truth.items():
+        dev = FakeShardDevice(t)
+        valid, local = verify_sharded(dev, {"jobs": shards[rank]}, dist)
+        full = gather_job_results(local, shards, len(t), dist)
+        out[name] = (valid, full.tolist(), dev.finished)
+    q.put((rank, out))
     dist.destroy_process_group()
 
 
-@pytest.mark.timeout(120)
-def test_allgather_partials_gloo_world2():
+@pytest.mark.timeout(180)
+def test_sharded_verdicts_gloo_world2():
     world = 2
+    truth = {
+        "all_valid": [1] * 10,
+        "one_false": [1, 1, 1, 1, 1, 1, 0, 1, 1, 1],       # a wrong-message block on one shard
+        "rejected_and_false": [1, -3, 1, 1, 1, 1, 1, 1, 0, 1],  # a not-in-G2 block plus a false one
+        "rejected_only": [1, 1, 1, 1, -8, 1, 1, 1, 1, 1],   # parse error: pairing check still passes
+    }
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, truth)) for r in range(world)]
     for p in ps:
         p.start()
-    res = sorted(q.get(timeout=100) for _ in range(world))
+    res = dict(q.get(timeout=150) for _ in range(world))
     for p in ps:
         p.join(timeout=30)
-    for rank, firsts, lens, shard in res:
-        assert firsts == [1, 2]
-        assert lens == [576, 576]
-    assert sorted(res[0][3] + res[1][3]) == list(range(10))
+    for rank in range(world):
+        o = res[rank]
+        assert o["firsts"] == [1, 2] and o["lens"] == [576, 576]
+        for name, t in truth.items():
+            valid, full, finished = o[name]
+            assert full == t, (rank, name)
+            want_valid = all(x == 1 or x < 0 for x in t)
+            assert valid == want_valid
+            assert finished == (0 if want_valid else 1)  # localisation only after a failed combined check
+    assert sorted(res[0]["shard"] + res[1]["shard"]) == list(range(10))
+
+
+def test_select_jobs_rebases_offsets():
+    from lodestar_amd.dist import select_jobs
+    arrays = {"n_sets": 5, "n_jobs": 3, "job_offsets": np.array([0, 2, 3, 5], np.uint32),
+              "pk_offsets": np.array([0, 2, 3, 6, 7, 9], np.uint32),
+              "pk_indices": np.arange(9, dtype=np.uint32) + 100,
+              "msgs": np.arange(5 * 32, dtype=np.uint8).reshape(5, 32),
+              "sigs": np.zeros((5, 192), np.uint8), "sig_len": np.full(5, 96, np.uint32), "n_raw": 0}
+    sub = select_jobs(arrays, [0, 2])
+    assert sub["n_sets"] == 4 and sub["n_jobs"] == 2
+    assert sub["job_offsets"].tolist() == [0, 2, 4]
+    assert sub["pk_offsets"].tolist() == [0, 2, 3, 4, 6]
+    assert sub["pk_indices"].tolist() == [100, 101, 102, 106, 107, 108]
+    assert (sub["msgs"] == arrays["msgs"][[0, 1, 3, 4]]).all()

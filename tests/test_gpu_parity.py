@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 def dev():
     from lodestar_amd import native
     d = native.Device(0)
-    d.pubkeys_set(0, G.interop_pubkeys48(), native.PK_COMPRESSED_48)
+    G.load_golden_table(d)
     yield d
     d.close()
 
@@ -43,7 +43,7 @@ def test_golden_batch_all_jobs(dev):
     assert st.batch_retries == 1  # the batch holds invalid jobs
 
 
-@pytest.mark.parametrize("job", list(range(16)))
+@pytest.mark.parametrize("job", list(range(len(G.batch_vectors()["jobs"]))))
 def test_golden_each_job_alone(dev, job):
     arrays, expected, codes = G.golden_arrays([job])
     jr, sc = dev.verify(arrays)
@@ -75,14 +75,48 @@ def test_partial_combine_matches_verify(dev):
     valid = [0, 1, 9, 11]
     a0, _, _ = G.golden_arrays(valid[:2])
     a1, _, _ = G.golden_arrays(valid[2:])
-    p0, _, ok0 = dev.partial(a0)
-    p1, _, ok1 = dev.partial(a1)
+    p0, _, _, ok0 = dev.partial(a0)
+    p1, _, _, ok1 = dev.partial(a1)
     assert ok0 and ok1
     assert dev.combine_final([p0, p1])
     bad, _, _ = G.golden_arrays([2])  # wrong-message job
-    p2, _, ok2 = dev.partial(bad)
+    p2, _, _, ok2 = dev.partial(bad)
     assert ok2
     assert not dev.combine_final([p0, p1, p2])
+
+
+def test_sharded_localisation_matches_verify(dev):
+    """SURVEY §8e "Failure": the golden batch split into 3 shards of whole
+    jobs; partial -> combined check -> (on failure) bgv_partial_finish per
+    shard gives exactly bgv_verify's per-job verdicts, and a shard whose own
+    check passes does not retry per job."""
+    from lodestar_amd.dist import select_jobs, shard_jobs
+    arrays, expected, _ = G.golden_arrays()
+    jo = arrays["job_offsets"]
+    shards = shard_jobs([int(jo[j + 1] - jo[j]) for j in range(arrays["n_jobs"])], 3)
+    parts, provisional = [], []
+    for ids in shards:
+        p, _, jr, _ = dev.partial(select_jobs(arrays, ids))
+        parts.append(p)
+        provisional.append(jr)
+    assert not dev.combine_final(parts)  # the golden batch holds false jobs
+    got = np.zeros(arrays["n_jobs"], np.int32)
+    for ids, prov in zip(shards, provisional):
+        sub = select_jobs(arrays, ids)
+        dev.partial(sub)
+        local = dev.partial_finish()
+        want = [expected[j] for j in ids]
+        assert local.tolist() == want
+        assert [int(x) if x < 0 else 1 for x in prov] == [w if w < 0 else 1 for w in want]
+        assert dev.last_stats.batch_retries == (1 if 0 in want else 0)
+        got[np.asarray(ids)] = local
+    assert got.tolist() == expected
+    # finish without a partial before it is refused
+    from lodestar_amd import native
+    dev.verify(G.golden_arrays([0])[0])
+    with pytest.raises(native.BgvNativeError) as e:
+        dev.partial_finish()
+    assert e.value.status == native.BGV_E_STATE
 
 
 def test_gen_keys_and_sign_match_oracle(dev):
@@ -195,9 +229,9 @@ def test_cooperative_miller_bit_identical_to_serial(monkeypatch):
         monkeypatch.setenv("BGV_MILLER", mode)
         d = native.Device(0)
         try:
-            d.pubkeys_set(0, G.interop_pubkeys48(), native.PK_COMPRESSED_48)
+            G.load_golden_table(d)
             a, expected, _ = G.golden_arrays([0, 1, 9, 11, 12, 13], scalars_seed=3)
-            part, _, ok = d.partial(a)
+            part, _, _, ok = d.partial(a)
             jr, _ = d.verify(G.golden_arrays(scalars_seed=3)[0])
             d.gen_keys(1000, 256, 5)
             syn, bad = _synthetic_on(d, 200, 8, 1000, 256, 9, fault_every=17)
@@ -311,9 +345,9 @@ def test_signature_msm_bit_identical_to_per_set_scaling(monkeypatch):
         monkeypatch.setenv("BGV_MSM", mode)
         d = native.Device(0)
         try:
-            d.pubkeys_set(0, G.interop_pubkeys48(), native.PK_COMPRESSED_48)
+            G.load_golden_table(d)
             a, _, _ = G.golden_arrays([0, 1, 9, 10, 11, 12, 13], scalars_seed=5)
-            part, _, ok = d.partial(a)
+            part, _, _, ok = d.partial(a)
             arrays, expected, codes = G.golden_arrays(scalars_seed=5)
             jr, sc = d.verify(arrays)
             assert jr.tolist() == expected and sc.tolist() == codes
@@ -321,7 +355,7 @@ def test_signature_msm_bit_identical_to_per_set_scaling(monkeypatch):
             syn, bad = _synthetic_on(d, 300, 8, 1000, 256, 4, fault_every=23)
             syn["n_jobs"] = 3
             syn["job_offsets"] = np.array([0, 100, 200, 300], np.uint32)
-            syn_part, _, _ = d.partial(syn)
+            syn_part, _, _, _ = d.partial(syn)
             jr2, _ = d.verify(syn)
             assert jr2.tolist() == [int(not bad[i * 100:(i + 1) * 100].any()) for i in range(3)]
             outs[mode] = (part, ok, syn_part)
@@ -343,9 +377,9 @@ def test_latency_split_mode_bit_identical(monkeypatch):
         monkeypatch.setenv("BGV_SPLIT", mode)
         d = native.Device(0)
         try:
-            d.pubkeys_set(0, G.interop_pubkeys48(), native.PK_COMPRESSED_48)
+            G.load_golden_table(d)
             a, expected, codes = G.golden_arrays([0, 1, 9, 11, 12, 13], scalars_seed=3)
-            part, _, ok = d.partial(a)
+            part, _, _, ok = d.partial(a)
             ga, gexp, gcodes = G.golden_arrays(scalars_seed=3)
             jr, sc = d.verify(ga)
             d.gen_keys(1000, 256, 5)
@@ -382,7 +416,7 @@ def test_two_level_job_fold_bit_identical(monkeypatch):
                 syn, bad = _synthetic_on(d, 300, 8, 1000, 256, 21, fault_every=fault_every)
                 syn["n_jobs"] = len(offs) - 1
                 syn["job_offsets"] = np.array(offs, np.uint32)
-                part, _, ok = d.partial(syn)
+                part, _, _, ok = d.partial(syn)
                 jr, _ = d.verify(syn)
                 want = [int(not bad[offs[j]:offs[j + 1]].any()) for j in range(len(offs) - 1)]
                 assert jr.tolist() == want

@@ -1,0 +1,113 @@
+"""GPU parity of the per-stage intermediates (SURVEY §8c golden plan): every
+stage of the HIP pipeline, read back through the test-only ABI entry
+bgv_debug_stages, is byte-identical to the oracle's value in
+tests/golden/batch_vectors.json (tools/gen_golden.py):
+
+  decoded signature, H(m), aggregated pubkey, r_i * pubkey   (affine points)
+  GT value of every set pair and every (-G1, S_job) pair    (FE of the Miller value)
+  S_job = sum r_i sigma_i, GT value of every job product and of the batch
+
+Miller values themselves are not canonical (projective line scalings differ
+by factors the final exponentiation kills), so pairs are compared after it.
+The device FE computes the cube of the textbook value, and the golden values
+are e(P, Q)^3.  Each pipeline variant a batch can take is compared:
+latency mode (two-lane hash maps, cooperative G2 and Miller), the bulk
+one-lane kernels, the bulk Miller kernel with one and with two pairs per work
+item, and the per-job Pippenger MSM for S_job.
+"""
+import numpy as np
+import pytest
+
+from oracle import bls12_381 as B
+from tests import gpu_util as G
+from tests.hostcheck import b_tower
+
+pytestmark = pytest.mark.gpu
+
+MODES = {
+    "latency": {},
+    "bulk": {"BGV_SPLIT": "0"},
+    "bulk_serial_msm": {"BGV_SPLIT": "0", "BGV_MILLER": "serial", "BGV_MSM": "1", "BGV_PAIRS": "1"},
+    "c4_path": {"BGV_SPLIT": "0", "BGV_MILLER": "serial", "BGV_MSM": "1", "BGV_PAIRS": "2"},
+}
+
+
+def _flat(gt_bytes: bytes):
+    return B.tower_to_f12(b_tower(gt_bytes))
+
+
+def _golden_gt(hexstr: str):
+    return tuple(int(hexstr[96 * k: 96 * k + 96], 16) for k in range(12))
+
+
+@pytest.fixture(scope="module")
+def golden():
+    v = G.batch_vectors()
+    sets = [s for j in v["jobs"] for s in j["sets"]]
+    return v, sets
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+def test_stage_values_match_oracle(monkeypatch, golden, mode):
+    from lodestar_amd import native
+    v, sets = golden
+    for k, val in MODES[mode].items():
+        monkeypatch.setenv(k, val)
+    d = native.Device(0)
+    try:
+        G.load_golden_table(d)
+        arrays, expected, codes = G.golden_arrays()
+        out = d.debug_stages(arrays)
+    finally:
+        d.close()
+    n, J = arrays["n_sets"], arrays["n_jobs"]
+    assert out["job_result"].tolist() == expected
+    assert out["set_code"].tolist() == codes
+    for i, s in enumerate(sets):
+        assert out["sig_aff"][i].tobytes().hex() == s["sig_aff"], ("sig_aff", i)
+        assert out["h_aff"][i].tobytes().hex() == s["h_aff"], ("h_aff", i)
+        assert out["pk_agg"][i].tobytes().hex() == s["pk_agg"], ("pk_agg", i)
+        assert out["rpk_aff"][i].tobytes().hex() == s["rpk_aff"], ("rpk_aff", i)
+    for j, job in enumerate(v["jobs"]):
+        assert out["s_aff"][j].tobytes().hex() == job["s_aff"], ("s_aff", j)
+        assert B.f12_eq(_flat(out["job_fe"][j].tobytes()), _golden_gt(job["job_gt"])), ("job_gt", j)
+        assert B.f12_eq(_flat(out["pair_fe"][n + j].tobytes()), _golden_gt(job["job_pair_gt"])), ("job_pair", j)
+    assert B.f12_eq(_flat(out["batch_fe"].tobytes()), _golden_gt(v["batch_gt"]))
+    # set pairs: one Miller value per set, or (two pairs per work item) the
+    # item's product at its first set and the identity at its second; an item
+    # with a rejected pubkey contributes the identity
+    pairs = MODES[mode].get("BGV_PAIRS", "1") == "2"
+    jo = arrays["job_offsets"]
+    for j in range(J):
+        beg, end = int(jo[j]), int(jo[j + 1])
+        step = 2 if pairs else 1
+        for i in range(beg, end, step):
+            grp = list(range(i, min(i + step, end)))
+            want = B.F12_ONE
+            if all(sets[k]["pk_agg"] != "00" * 96 for k in grp):  # no rejected pubkey in the item
+                for k in grp:
+                    want = B.f12_mul(want, _golden_gt(sets[k]["pair_gt"]))
+            assert B.f12_eq(_flat(out["pair_fe"][i].tobytes()), want), ("pair", i)
+            for k in grp[1:]:
+                assert B.f12_eq(_flat(out["pair_fe"][k].tobytes()), B.F12_ONE), ("pair2", k)
+
+
+def test_stage_values_independent_of_batching(golden):
+    """the same job alone and inside the full batch: identical stage values
+    (each set's values depend only on its own inputs and scalar)"""
+    from lodestar_amd import native
+    v, sets = golden
+    d = native.Device(0)
+    try:
+        G.load_golden_table(d)
+        full = d.debug_stages(G.golden_arrays()[0])
+        first = 0
+        for j, job in enumerate(v["jobs"]):
+            one = d.debug_stages(G.golden_arrays([j])[0])
+            k = len(job["sets"])
+            for key in ("sig_aff", "h_aff", "pk_agg", "rpk_aff"):
+                assert (one[key][:k] == full[key][first:first + k]).all(), (key, j)
+            assert (one["s_aff"][0] == full["s_aff"][j]).all() if v["jobs"][j]["sets"] else True
+            first += k
+    finally:
+        d.close()

@@ -9,6 +9,16 @@ packages/beacon-node/test/e2e/chain/bls/multithread.test.ts:25-38
 Expected verdicts / errors are computed by oracle.verify_job, i.e. the
 reference's maybeBatch semantics restated.
 
+Every set also carries its batch scalar and the canonical per-stage values
+the device must reproduce (SURVEY §8c golden plan; compared on the GPU by
+tests/test_gpu_stages.py through bgv_debug_stages): the decoded signature,
+H(m), the aggregated pubkey, r * pubkey, and the GT value of its Miller pair;
+every job its S_job = sum r_i sigma_i and the GT value of its product.  GT
+values are e(P, Q)^3 (the device's final exponentiation computes the cube of
+the textbook value, include/bgv.h bgv_debug) as 12 flat coefficients of
+oracle.f12 (Fp[w]/(w^12 - 2 w^6 + 2)).  Points: G1 x || y, G2 x.c0 || x.c1
+|| y.c0 || y.c1, 48-byte big-endian, all-zero for the identity / rejected.
+
     python tools/gen_golden.py
 """
 import hashlib
@@ -56,22 +66,59 @@ def not_in_group_sig():
         x0 += 1
 
 
+TABLE_BASE = 100  # extra_table rows follow the 100 interop keys
+INDEX_RANGE = 9   # include/bgv.h BGV_SET_INDEX_RANGE: index2pubkey[i] undefined on the caller's side
+
+
+def scalar(i):
+    """batch scalar of golden set i (64-bit, non-zero)"""
+    return int.from_bytes(hashlib.sha256(b"golden-scalar" + i.to_bytes(4, "little")).digest()[:8], "little") | 1
+
+
+def fp_b(v):
+    return (v % B.P).to_bytes(48, "big")
+
+
+def g1_b(pt):
+    return bytes(96) if pt is None else fp_b(pt[0]) + fp_b(pt[1])
+
+
+def g2_b(pt):
+    return bytes(192) if pt is None else b"".join(fp_b(c) for c in (pt[0][0], pt[0][1], pt[1][0], pt[1][1]))
+
+
+def gt_hex(f):
+    return "".join(fp_b(c).hex() for c in f)
+
+
+def cube(f):
+    return B.f12_mul(B.f12_mul(f, f), f)
+
+
 def main():
     interop = json.load(open(os.path.join(ROOT, "tests", "golden", "interop-pubkeys.json")))
     sks = [B.interop_secret_key(i) for i in range(len(interop))]
     pts = {}
+    # rows appended after the interop keys (uncompressed 96 B): -P_24, the identity
+    neg24 = B.E1.neg(B.g1_decompress(bytes.fromhex(interop[24][2:]))[1])
+    extra_table = [B.g1_serialize(neg24), bytes([0x40]) + bytes(95)]
+    extra_pts = {TABLE_BASE: neg24, TABLE_BASE + 1: None}
 
     def pk_point(idxs):
         acc = None
         for i in idxs:
+            if i >= TABLE_BASE:
+                acc = B.E1.add(acc, extra_pts[i])
+                continue
             if i not in pts:
                 pts[i] = B.g1_decompress(bytes.fromhex(interop[i][2:]))[1]
             acc = B.E1.add(acc, pts[i])
         return acc
 
-    # raw keys of multithread.test.ts:25-38
+    # raw keys of multithread.test.ts:25-38, then the uncompressed identity (raw key 3)
     raw_sks = [int.from_bytes(bytes([k + 1]) * 32, "big") % B.R for k in range(3)]
-    raw_pks = [B.g1_serialize(B.sk_to_pk(s)) for s in raw_sks]
+    raw_pks = [B.g1_serialize(B.sk_to_pk(s)) for s in raw_sks] + [bytes([0x40]) + bytes(95)]
+    raw_pts = [B.sk_to_pk(s) for s in raw_sks] + [None]
 
     jobs = []  # list of list of set dicts
 
@@ -123,34 +170,109 @@ def main():
     jobs.append([S([23], m=msg(21), sig=bytes(u))])
     # J15: empty job (chunkify of [] = [[]]) -> "Empty signature set"
     jobs.append([])
+    # J16: P + (-P) aggregates to the identity -> BLST_PK_IS_INFINITY (blst
+    # Pairing.mul_n_aggregate); the signature is the identity (sk sum 0)
+    jobs.append([S([25], m=msg(30), sig=agg_sig([sks[25]], msg(30))),
+                 S([24, TABLE_BASE], m=msg(31), sig=bytes([0xC0]) + bytes(95))])
+    # J17: a valid set, then a set whose only (raw) key is the identity -> BLST_PK_IS_INFINITY
+    jobs.append([S([26], m=msg(32), sig=agg_sig([sks[26]], msg(32))),
+                 S(raw=3, m=msg(33), sig=agg_sig([sks[27]], msg(33)))])
+    # J18: a pubkey index past the table -> rejected per set (BGV_INDEX_RANGE); the
+    # reference's index2pubkey[i] is undefined and the caller throws
+    jobs.append([S([28], m=msg(34), sig=agg_sig([sks[28]], msg(34))),
+                 S([29, 5000], m=msg(35), sig=agg_sig([sks[29]], msg(35)))])
+    # J19: 192-byte signature with the sign flag (0x20) -> BAD_ENCODING
+    u = bytearray(B.g2_serialize(B.sign(sks[30], msg(36))))
+    u[0] |= 0x20
+    jobs.append([S([30], m=msg(36), sig=bytes(u))])
+    # J20: precedence: set 0's pubkeys sum to the identity, set 1's signature
+    # does not decode -> every signature is parsed first (maybeBatch.ts:20-24):
+    # BAD_ENCODING, not PK_IS_INFINITY
+    jobs.append([S([24, TABLE_BASE], m=msg(37), sig=bytes([0xC0]) + bytes(95)),
+                 S([31], m=msg(38), sig=bytes(xp))])
+    # J21: two valid sets on the appended rows' neighbours, one key repeated
+    # across sets (a 2-set batch, non-trivial S_job)
+    jobs.append([S([32, 33, 34], m=msg(39), sig=agg_sig([sks[32], sks[33], sks[34]], msg(39))),
+                 S([34], m=msg(40), sig=agg_sig([sks[34]], msg(40)))])
 
     out_jobs = []
+    set_no = 0
+    batch_gt = B.F12_ONE
+    neg_g1 = B.E1.neg(B.G1)
     for jid, job in enumerate(jobs):
-        sets = []
+        sets, inter = [], []
+        range_err = False
         for s in job:
-            pkp = pk_point(s["pk"]) if s["raw"] is None else B.sk_to_pk(raw_sks[s["raw"]])
+            if s["raw"] is not None:
+                pkp = raw_pts[s["raw"]]
+            elif any(i >= TABLE_BASE + len(extra_table) for i in s["pk"]):
+                pkp, range_err = None, True
+            else:
+                pkp = pk_point(s["pk"])
             sets.append((pkp, s["msg"], s["sig"]))
-        try:
-            verdict = 1 if B.verify_job(sets) else 0
-        except B.BlstError as e:
-            verdict = -e.code
-        except ValueError:
-            verdict = -10
-        codes = []
+        codes, sig_pts = [], []
         for s in job:
             try:
-                B.signature_from_bytes(s["sig"], True)
+                sig_pts.append(B.signature_from_bytes(s["sig"], True))
                 codes.append(0)
             except B.BlstError as e:
+                sig_pts.append(None)
                 codes.append(e.code)
+        for k, s in enumerate(job):  # device set code: signature code, else pubkey code
+            if codes[k] == 0:
+                if s["raw"] is None and any(i >= TABLE_BASE + len(extra_table) for i in s["pk"]):
+                    codes[k] = INDEX_RANGE
+                elif sets[k][0] is None:
+                    codes[k] = B.BLST_PK_IS_INFINITY
+        sig_codes = [c if c not in (INDEX_RANGE, B.BLST_PK_IS_INFINITY) else 0 for c in codes]
+        if range_err and not any(sig_codes):
+            verdict = -INDEX_RANGE
+        else:
+            try:
+                verdict = 1 if B.verify_job(sets) else 0
+            except B.BlstError as e:
+                verdict = -e.code
+            except ValueError:
+                verdict = -10
+        job_ok = verdict >= 0
+        s_acc = None
+        job_gt = B.F12_ONE
+        for k, s in enumerate(job):
+            r = scalar(set_no + k)
+            pkp = sets[k][0]
+            h = B.hash_to_g2(s["msg"])
+            rpk = B.E1.mul(pkp, r) if pkp is not None else None
+            pair = cube(B.pairing(rpk, h)) if rpk is not None else B.F12_ONE
+            inter.append({"scalar": str(r), "sig_aff": g2_b(sig_pts[k]).hex(), "h_aff": g2_b(h).hex(),
+                          "pk_agg": g1_b(pkp).hex(), "rpk_aff": g1_b(rpk).hex(), "pair_gt": gt_hex(pair)})
+            if job_ok:
+                if sig_pts[k] is not None:
+                    s_acc = B.E2.add(s_acc, B.E2.mul(sig_pts[k], r))
+                job_gt = B.f12_mul(job_gt, pair)
+        job_pair = B.F12_ONE
+        if job_ok and s_acc is not None:
+            job_pair = cube(B.pairing(neg_g1, s_acc))
+            job_gt = B.f12_mul(job_gt, job_pair)
+        if not job_ok:
+            s_acc = None
+            job_gt = B.F12_ONE
+        batch_gt = B.f12_mul(batch_gt, job_gt)
+        assert (verdict == 1) == (job_ok and B.f12_eq(job_gt, B.F12_ONE)) or verdict < 0
+        set_no += len(job)
         out_jobs.append({
             "expected": verdict,
-            "sets": [{"pk": s["pk"], "raw": s["raw"], "msg": s["msg"].hex(), "sig": s["sig"].hex(), "code": c}
-                     for s, c in zip(job, codes)],
+            "s_aff": g2_b(s_acc).hex(),
+            "job_pair_gt": gt_hex(job_pair),
+            "job_gt": gt_hex(job_gt),
+            "sets": [dict({"pk": s["pk"], "raw": s["raw"], "msg": s["msg"].hex(), "sig": s["sig"].hex(), "code": c}, **it)
+                     for s, c, it in zip(job, codes, inter)],
         })
         print(jid, verdict, codes, flush=True)
     json.dump({"generator": "tools/gen_golden.py (oracle/bls12_381.py)",
-               "raw_pubkeys": [p.hex() for p in raw_pks], "jobs": out_jobs}, open(OUT, "w"), indent=1)
+               "gt_note": "GT values are e(P, Q)^3 as 12 flat coefficients of oracle.f12 (Fp[w]/(w^12 - 2 w^6 + 2))",
+               "raw_pubkeys": [p.hex() for p in raw_pks], "extra_table_base": TABLE_BASE,
+               "extra_table": [p.hex() for p in extra_table], "batch_gt": gt_hex(batch_gt),
+               "jobs": out_jobs}, open(OUT, "w"), indent=1)
     print("wrote", OUT)
 
 
