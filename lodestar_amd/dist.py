@@ -51,10 +51,12 @@ def select_jobs(arrays: dict, jobs: list[int]) -> dict:
     out["job_offsets"] = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
     out["pk_offsets"] = np.concatenate([[0], np.cumsum(k)]).astype(np.uint32)
     out["pk_indices"] = np.asarray(arrays["pk_indices"])[idx].astype(np.uint32) if len(idx) else np.zeros(1, np.uint32)
-    for key in ("msgs", "sigs", "sig_len", "scalars"):
+    n = int(arrays["n_sets"])
+    for key, width in (("msgs", 32), ("sigs", 192), ("sig_len", 1), ("scalars", 1)):
         v = arrays.get(key)
-        if v is not None:
-            out[key] = np.asarray(v)[sets].copy() if len(sets) else np.asarray(v)[:1].copy()
+        if v is not None:  # flat byte arrays and (n, width) arrays alike
+            rows = np.asarray(v)[: max(n, 1) * width].reshape(max(n, 1), width) if width > 1 else np.asarray(v)
+            out[key] = rows[sets].copy() if len(sets) else rows[:1].copy()
     return out
 
 

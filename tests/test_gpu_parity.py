@@ -233,8 +233,9 @@ def test_cooperative_miller_bit_identical_to_serial(monkeypatch):
             a, expected, _ = G.golden_arrays([0, 1, 9, 11, 12, 13], scalars_seed=3)
             part, _, _, ok = d.partial(a)
             jr, _ = d.verify(G.golden_arrays(scalars_seed=3)[0])
-            d.gen_keys(1000, 256, 5)
-            syn, bad = _synthetic_on(d, 200, 8, 1000, 256, 9, fault_every=17)
+            first = d.pubkeys_count()
+            d.gen_keys(first, 256, 5)
+            syn, bad = _synthetic_on(d, 200, 8, first, 256, 9, fault_every=17)
             jr2, _ = d.verify(syn)
             outs[mode] = (part, ok, jr.tolist(), jr2.tolist(), bad)
         finally:
@@ -351,8 +352,9 @@ def test_signature_msm_bit_identical_to_per_set_scaling(monkeypatch):
             arrays, expected, codes = G.golden_arrays(scalars_seed=5)
             jr, sc = d.verify(arrays)
             assert jr.tolist() == expected and sc.tolist() == codes
-            d.gen_keys(1000, 256, 5)
-            syn, bad = _synthetic_on(d, 300, 8, 1000, 256, 4, fault_every=23)
+            first = d.pubkeys_count()
+            d.gen_keys(first, 256, 5)
+            syn, bad = _synthetic_on(d, 300, 8, first, 256, 4, fault_every=23)
             syn["n_jobs"] = 3
             syn["job_offsets"] = np.array([0, 100, 200, 300], np.uint32)
             syn_part, _, _, _ = d.partial(syn)
@@ -382,8 +384,9 @@ def test_latency_split_mode_bit_identical(monkeypatch):
             part, _, _, ok = d.partial(a)
             ga, gexp, gcodes = G.golden_arrays(scalars_seed=3)
             jr, sc = d.verify(ga)
-            d.gen_keys(1000, 256, 5)
-            syn, bad = _synthetic_on(d, 200, 8, 1000, 256, 9, fault_every=17)
+            first = d.pubkeys_count()
+            d.gen_keys(first, 256, 5)
+            syn, bad = _synthetic_on(d, 200, 8, first, 256, 9, fault_every=17)
             jr2, _ = d.verify(syn)
             outs[mode] = (part, ok, jr.tolist(), sc.tolist(), jr2.tolist(), bad)
         finally:
@@ -410,10 +413,11 @@ def test_two_level_job_fold_bit_identical(monkeypatch):
         monkeypatch.setenv("BGV_PREFOLD", mode)
         d = native.Device(0)
         try:
-            d.gen_keys(1000, 256, 5)
+            first = d.pubkeys_count()
+            d.gen_keys(first, 256, 5)
             res = []
             for fault_every in (0, 150):  # 150: faults at sets 0 and 150 (jobs 0 and 1)
-                syn, bad = _synthetic_on(d, 300, 8, 1000, 256, 21, fault_every=fault_every)
+                syn, bad = _synthetic_on(d, 300, 8, first, 256, 21, fault_every=fault_every)
                 syn["n_jobs"] = len(offs) - 1
                 syn["job_offsets"] = np.array(offs, np.uint32)
                 part, _, _, ok = d.partial(syn)

@@ -104,7 +104,7 @@ def test_pubkey_table_mirror_errors():
         assert len(pool.table) == 20 and pool.table.pubkey2index[keys[19]] == 19
         pool.table.sync_pubkeys(keys[:40])  # appends 20..39 only
         assert len(pool.table) == 40
-        bad = bytes([0x80]) + b"\xff" * 47  # x >= p
+        bad = bytes([0x9F]) + b"\xff" * 47  # x >= p
         with pytest.raises(V.BlsError, match="BLST_BAD_ENCODING"):
             pool.table.sync_pubkeys(keys[:40] + [bad])
         assert len(pool.table) == 40
