@@ -446,16 +446,20 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   const uint32_t total = c->pk_total;
   // grid bound of the chunked pubkey gather: sum ceil(k_i/32) <= total/32 + n
   d.chunk_bound = total / 32 + n;
-  // two pairs per Miller work item only when the batch alone fills the chip
-  // (>= 65536 sets ~ 2 waves per SIMD at 1 pair per lane); below that the
-  // per-lane latency of a longer item dominates
-  d.pairs_per_item = n >= 65536 ? 2 : 1;
+  // Pipeline variant by batch size, from the r02 sweep of on-device C4-shaped
+  // batches (tools/sweep_modes.py):
+  //  * cooperative Miller loop (36 lanes per pair) below MILLER_COOP_MAX sets;
+  //    above it the one-lane loop (36x fewer lanes) wins: 7,840 sets 20.1 ->
+  //    18.2 ms, 12,544 sets 28.6 -> 20.0 ms, 50,176 sets 95.6 -> 29.3 ms;
+  //  * per-job bucket MSM for sum r_i sigma_i from the same size (its 16
+  //    lanes per job lengthen small batches: 98 sets 7.1 -> 17 ms);
+  //  * latency mode (two-lane hash maps, cooperative G2) below SPLIT_MAX
+  //    (25,088 sets: 24.5 ms split against 26.3 ms; 50,176: 35.4 against 29.3);
+  //  * two pairs per Miller work item only when the batch alone fills the chip.
+  static const uint32_t MILLER_COOP_MAX = 6000, SPLIT_MAX = 35000, PAIRS2_MIN = 65536;
+  d.pairs_per_item = n >= PAIRS2_MIN ? 2 : 1;
   if (c->pairs == 1 || c->pairs == 2) d.pairs_per_item = (uint32_t)c->pairs;
-  // latency mode below one chip-full of lanes: hash maps on two lanes per
-  // set, subgroup check beside the signature scaling (bgv_kernels.hip)
-  d.split = c->split >= 0 ? (uint32_t)c->split : (n < 65536 ? 1u : 0u);
-  // cooperative Miller loop (36 lanes per pair, low latency) unless the batch alone
-  // fills the GPU, where the one-lane loop does less work per pair
+  d.split = c->split >= 0 ? (uint32_t)c->split : (n < SPLIT_MAX ? 1u : 0u);
   // two-level per-job fold (bgv_tail.hip) when few jobs of >= 64 sets leave
   // the chip idle: groups of ~sqrt(span) sets fold side by side, then the job
   // folds the group values, 2 sqrt(span) sequential Fp12 products instead of span
@@ -464,12 +468,11 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
     const bool on = c->prefold >= 0 ? (c->prefold && d.span_log2 >= 2 && d.span_log2 <= 8) : few_big;
     d.prefold_log2 = on ? (d.span_log2 + 1) / 2 : 0u;
   }
-  d.miller_coop = c->miller_mode >= 0 ? (uint32_t)c->miller_mode : (n < 65536 ? 1u : 0u);
+  d.miller_coop = c->miller_mode >= 0 ? (uint32_t)c->miller_mode : (n < MILLER_COOP_MAX ? 1u : 0u);
   // sum r_i sigma_i per job by a bucket MSM (16 x 4-bit windows, ~1,800 G2
   // additions per 98-set job instead of 98 x 75 in per-set scalar mults)
-  // when the batch fills the GPU and jobs are block-sized; small batches keep
-  // the per-set path, whose latency is one 64-bit scalar mult
-  d.msm = c->msm_mode >= 0 ? (uint32_t)c->msm_mode : ((n >= 65536 && d.span_log2 <= 8) ? 1u : 0u);
+  // when jobs are block-sized (<= 256 sets)
+  d.msm = c->msm_mode >= 0 ? (uint32_t)c->msm_mode : ((n >= MILLER_COOP_MAX && d.span_log2 <= 8) ? 1u : 0u);
   if (b->scalars && !b->on_device) {
     // staged with the other host arrays above
   } else if (b->scalars) {
