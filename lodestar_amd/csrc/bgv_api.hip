@@ -62,7 +62,8 @@ struct dbuf {
 
 struct bgv_ctx {
   int device = 0;
-  int miller_mode = -1;  // BGV_MILLER=serial|coop forces one Miller kernel (A/B tests); -1 = by batch size
+  int miller_mode = -1;  // BGV_MILLER=serial|coop|6|18|36 forces the set-pair Miller layout (A/B tests); -1 = by batch size
+  int job_lanes = 0;     // BGV_JOB_LANES=6|18|36: layout of the (-G1, S_job) pairs; 0 = default
   int msm_mode = -1;     // BGV_MSM=0|1 forces the signature combination (A/B tests); -1 = by batch shape
   bool overlap = true;    // BGV_OVERLAP=0 runs every stage on one stream (A/B tests)
   int split = -1;         // BGV_SPLIT=0|1 forces the latency mode (A/B tests); -1 = by batch size
@@ -166,7 +167,10 @@ int bgv_open(int device, bgv_ctx** out) {
   HIPCHK(hipSetDevice(device));
   bgv_ctx* c = new bgv_ctx();
   c->device = device;
-  if (const char* m = getenv("BGV_MILLER")) c->miller_mode = strcmp(m, "serial") != 0 ? 1 : 0;
+  // BGV_MILLER=serial | coop (36 lanes per pair) | 6 | 18 | 36
+  if (const char* m = getenv("BGV_MILLER"))
+    c->miller_mode = strcmp(m, "serial") == 0 ? 0 : (atoi(m) == 6 || atoi(m) == 18) ? atoi(m) : 36;
+  if (const char* m = getenv("BGV_JOB_LANES")) c->job_lanes = (atoi(m) == 6 || atoi(m) == 18) ? atoi(m) : 36;
   if (const char* m = getenv("BGV_MSM")) c->msm_mode = strcmp(m, "0") != 0 ? 1 : 0;
   if (const char* o = getenv("BGV_OVERLAP")) c->overlap = strcmp(o, "0") != 0;
   if (const char* o = getenv("BGV_PAIRS")) c->pairs = atoi(o);
@@ -468,7 +472,8 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
     const bool on = c->prefold >= 0 ? (c->prefold && d.span_log2 >= 2 && d.span_log2 <= 8) : few_big;
     d.prefold_log2 = on ? (d.span_log2 + 1) / 2 : 0u;
   }
-  d.miller_coop = c->miller_mode >= 0 ? (uint32_t)c->miller_mode : (n < MILLER_COOP_MAX ? 1u : 0u);
+  d.miller_coop = c->miller_mode >= 0 ? (uint32_t)c->miller_mode : (n < MILLER_COOP_MAX ? 36u : 0u);
+  d.job_lanes = c->job_lanes ? (uint32_t)c->job_lanes : 36u;
   // sum r_i sigma_i per job by a bucket MSM (16 x 4-bit windows, ~1,800 G2
   // additions per 98-set job instead of 98 x 75 in per-set scalar mults)
   // when jobs are block-sized (<= 256 sets)

@@ -18,7 +18,9 @@ struct dev_batch {
   uint32_t n_sets, n_jobs, n_raw, table_n;
   uint32_t span_log2;    // per-job reduction tree covers 2^span_log2 sets
   uint32_t chunk_bound;  // upper bound of pubkey chunks (grid of k_pk_chunk)
-  uint32_t miller_coop;     // 1: cooperative Miller loop (miller_coop.h, 36 lanes per pair)
+  uint32_t miller_coop;     // set pairs: 0 one-lane Miller loop (k_miller), else lanes per pair of the
+                            // cooperative loop (miller_coop.h: 6, 18 or 36)
+  uint32_t job_lanes;       // (-G1, S_job) pairs: lanes per pair of the cooperative loop (6, 18 or 36)
   uint32_t pairs_per_item;  // Miller pairs sharing one accumulator (1, or 2 for batches that fill the GPU)
   uint32_t msm;             // 1: per-job bucket MSM for sum r_i sigma_i (k_msm_*), 0: per-set [r_i] sigma_i + tree
   uint32_t split;           // 1: latency mode: hash maps on two lanes per set, subgroup check beside [r_i] sigma_i

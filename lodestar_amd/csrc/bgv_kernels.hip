@@ -617,15 +617,18 @@ __global__ void BGV_BULK k_item_job(dev_batch b, dev_work w) {
 
 // k_miller (the set-pair Miller loops) lives in bgv_miller.hip (1 wave/SIMD).
 
-// Cooperative variant (miller_coop.h): COOP_GROUPS pairs per 64-lane
-// workgroup, 6 x COOP_SUB lanes per pair, pair t < n_sets is (r_t PK_t, H(m_t)), then (-G1, S_job).
+// Cooperative variant (miller_coop.h): GROUPS pairs per 64-lane workgroup,
+// 6 x SUB x HALF lanes per pair; pair t < n_sets is (r_t PK_t, H(m_t)), then
+// (-G1, S_job).
+template <int SUB, int HALF>
 __global__ void __launch_bounds__(64, BGV_WAVES) k_miller_coop(dev_batch b, dev_work w, uint32_t first, uint32_t count) {
-  __shared__ coop_grp sm[COOP_GROUPS];
-  const uint32_t lane = threadIdx.x, grp = lane / COOP_GROUP_LANES;
-  const uint32_t r = lane % COOP_GROUP_LANES;
-  const uint32_t k = r / (COOP_SUB * COOP_HALF), h = (r / COOP_SUB) % COOP_HALF, q = r % COOP_SUB;
-  const uint32_t t = first + blockIdx.x * COOP_GROUPS + grp;
-  const bool in_range = grp < COOP_GROUPS && t < first + count;
+  using cfg = coop_cfg<SUB, HALF>;
+  __shared__ coop_grp_t<SUB, HALF> sm[cfg::GROUPS];
+  const uint32_t lane = threadIdx.x, grp = lane / cfg::LANES;
+  const uint32_t r = lane % cfg::LANES;
+  const uint32_t k = r / (SUB * HALF), h = (r / SUB) % HALF, q = r % SUB;
+  const uint32_t t = first + blockIdx.x * cfg::GROUPS + grp;
+  const bool in_range = grp < cfg::GROUPS && t < first + count;
   bool active = in_range;
   if (in_range) {
     g1a P;
@@ -645,7 +648,7 @@ __global__ void __launch_bounds__(64, BGV_WAVES) k_miller_coop(dev_batch b, dev_
       Q = w.s_aff[j];
     }
     if (active && k == 0 && q == 0 && h == 0) {
-      coop_grp& g = sm[grp];
+      coop_grp_t<SUB, HALF>& g = sm[grp];
       g.T[0] = Q.x;
       g.T[1] = Q.y;
       g.T[2] = fp2_one();
@@ -658,7 +661,7 @@ __global__ void __launch_bounds__(64, BGV_WAVES) k_miller_coop(dev_batch b, dev_
     }
   }
   __syncthreads();
-  coop_miller(sm[grp < COOP_GROUPS ? grp : 0], k, h, q, active);
+  coop_miller<SUB, HALF>(sm[grp < cfg::GROUPS ? grp : 0], k, h, q, active);
   if (in_range && q == 0 && h == 0) {
     fp2_t v;
     if (active) v = sm[grp].f[k];
@@ -902,6 +905,23 @@ void launch_prep(hipStream_t st, const dev_batch& b, const dev_work& w) {
   }
 }
 
+// pairs [first, first + count) through the cooperative layout of `lanes`
+// lanes per pair (6, 18 or 36)
+static void launch_miller_coop(hipStream_t st, uint32_t lanes, const dev_batch& b, const dev_work& w, uint32_t first,
+                               uint32_t count) {
+  if (!count) return;
+  if (lanes == 6) {
+    constexpr uint32_t G = coop_cfg<1, 1>::GROUPS;
+    hipLaunchKernelGGL((k_miller_coop<1, 1>), dim3((count + G - 1) / G), dim3(64), 0, st, b, w, first, count);
+  } else if (lanes == 18) {
+    constexpr uint32_t G = coop_cfg<3, 1>::GROUPS;
+    hipLaunchKernelGGL((k_miller_coop<3, 1>), dim3((count + G - 1) / G), dim3(64), 0, st, b, w, first, count);
+  } else {
+    constexpr uint32_t G = coop_cfg<3, 2>::GROUPS;
+    hipLaunchKernelGGL((k_miller_coop<3, 2>), dim3((count + G - 1) / G), dim3(64), 0, st, b, w, first, count);
+  }
+}
+
 void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work& w) {
   const uint32_t span = 1u << b.span_log2;
   switch (stage) {
@@ -958,7 +978,7 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
     case ST_MILLER:  // (r_i PK_i, H(m_i)) pairs: needs ST_HASH and ST_PK only
       if (b.miller_coop) {
         if (b.n_sets)
-          hipLaunchKernelGGL(k_miller_coop, dim3((b.n_sets + COOP_GROUPS - 1) / COOP_GROUPS), dim3(64), 0, st, b, w, 0u, b.n_sets);
+          launch_miller_coop(st, b.miller_coop, b, w, 0u, b.n_sets);
         break;
       }
       launch_miller(st, b, w);  // bgv_miller.hip
@@ -968,7 +988,7 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       // lane takes ~19 ms at C4, the cooperative loop ~5 ms) and its waves
       // fit on the SIMDs the set-pair kernel leaves free
       if (b.n_jobs)
-        hipLaunchKernelGGL(k_miller_coop, dim3((b.n_jobs + COOP_GROUPS - 1) / COOP_GROUPS), dim3(64), 0, st, b, w, b.n_sets, b.n_jobs);
+        launch_miller_coop(st, b.job_lanes, b, w, b.n_sets, b.n_jobs);
       break;
     case ST_F_TREE:
       launch_fp12_tail(st, stage, b, w);  // bgv_tail.hip

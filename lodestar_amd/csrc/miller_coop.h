@@ -25,27 +25,25 @@
 
 namespace bgv {
 
-// BGV_COOP_SUB = 3: every coefficient lane k is three sub-lanes q, one per
-// Karatsuba Fp product of each Fp2 product (coop_prod_sub), so a product
-// round costs the latency of ONE Fp product instead of three.  18 lanes per
-// pair, 3 pairs per wave.  BGV_COOP_SUB = 1: the six-lane form.
-#ifndef BGV_COOP_SUB
-#define BGV_COOP_SUB 3
-#endif
-// BGV_COOP_HALF = 2 (with COOP_SUB = 3): every coefficient lane is also split
-// in two halves h that share the squaring's four products and the line
-// multiplication's three (2 + 2 and 2 + 1 per half), so those steps take 2
-// product rounds instead of 4 and 3.  36 lanes per pair, one pair per wave.
-#ifndef BGV_COOP_HALF
-#define BGV_COOP_HALF 2
-#endif
+// Layouts (template parameters SUB, HALF; the launcher picks one by batch
+// size, bgv_kernels.hip):
+//   SUB = 3: every coefficient lane k is three sub-lanes q, one per Karatsuba
+//     Fp product of each Fp2 product (coop_prod_sub), so a product round
+//     costs the latency of ONE Fp product instead of three;
+//   HALF = 2 (with SUB = 3): every coefficient lane is also split in two
+//     halves h that share the squaring's four products and the line
+//     multiplication's three (2 + 2 and 2 + 1 per half), so those steps take
+//     2 product rounds instead of 4 and 3;
+//   <1, 1> = 6 lanes per pair (10 pairs per wave), <3, 1> = 18 (3 per wave),
+//   <3, 2> = 36 (one pair per wave).
+template <int SUB, int HALF> struct coop_cfg {
+  static_assert((SUB == 1 && HALF == 1) || (SUB == 3 && (HALF == 1 || HALF == 2)), "coop layout");
+  static constexpr int LANES = 6 * SUB * HALF;  // lanes per pair
+  static constexpr int GROUPS = 64 / LANES;     // pairs per 64-lane workgroup
+};
 constexpr int COOP_LANES = 6;
-constexpr int COOP_SUB = BGV_COOP_SUB;
-constexpr int COOP_HALF = (BGV_COOP_SUB == 3) ? BGV_COOP_HALF : 1;
-constexpr int COOP_GROUP_LANES = COOP_LANES * COOP_SUB * COOP_HALF;
-constexpr int COOP_GROUPS = 64 / COOP_GROUP_LANES;  // 10 (60 of 64 lanes), 3 (54) or 1 (36)
 
-struct coop_grp {
+template <int SUB, int HALF> struct coop_grp_t {
   fp2_t f[6];     // w-basis coefficients of the accumulator
   fp2_t T[3];     // X, Y, Z (homogeneous projective)
   fp2_t Q[2];     // affine Q (addition steps)
@@ -53,13 +51,11 @@ struct coop_grp {
   fp2_t line[3];  // a0, a1, b1
   fp2_t r[8];     // per-round products
   fp2_t a[6];     // per-lane staged operand
-#if BGV_COOP_SUB == 3
-  fp_t P[6 * COOP_HALF][3];  // sub-lane Fp products of coefficient lane (k, h)
-#endif
-#if BGV_COOP_SUB == 3 && BGV_COOP_HALF == 2
-  fp2_t hs[6][2];  // per-half partial sums
-  fp2_t ah[6][2];  // per-half staged products
-#endif
+  // layout-specific exchange slots; zero-length (no LDS) where unused, so
+  // the 6-lane layout's 10 groups fit 5 workgroups per CU
+  fp_t P[SUB == 3 ? 6 * HALF : 0][3];  // sub-lane Fp products of coefficient lane (k, h)
+  fp2_t hs[HALF == 2 ? 6 : 0][2];      // per-half partial sums
+  fp2_t ah[HALF == 2 ? 6 : 0][2];      // per-half staged products
 };
 
 // f^2 by the symmetric schoolbook in the w-basis: lane k sums 4 products
@@ -133,16 +129,20 @@ __device__ __forceinline__ void coop_prod_sub(fp_t* P, uint32_t q, const fp2_t* 
   coop_wave_sync();
 }
 
-#if BGV_COOP_SUB == 3
-#define COOP_PROD(pa, pb, out) coop_prod_sub(g.P[k * COOP_HALF + h], q, (pa), (pb), (out))
-#else
-#define COOP_PROD(pa, pb, out) coop_prod((pa), (pb), (out))
-#endif
+// one Fp2 product of coefficient lane (k, h): over its three sub-lanes (SUB = 3) or alone
+template <int SUB, int HALF>
+__device__ __forceinline__ void cprod(coop_grp_t<SUB, HALF>& g, uint32_t k, uint32_t h, uint32_t q, const fp2_t* a,
+                                      const fp2_t* b, fp2_t* out) {
+  if constexpr (SUB == 3) coop_prod_sub(g.P[k * HALF + h], q, a, b, out);
+  else coop_prod(a, b, out);
+}
+#define COOP_PROD(pa, pb, out) cprod<SUB, HALF>(g, k, h, q, (pa), (pb), (out))
 
 // lanes 0..5: g.r[k] <- c_k of f * (a0 + a1 w^2 + b1 w^3); then f <- that
-__device__ __forceinline__ void coop_line_round(coop_grp& g, uint32_t k, uint32_t h, uint32_t q, bool active) {
+template <int SUB, int HALF>
+__device__ __forceinline__ void coop_line_round(coop_grp_t<SUB, HALF>& g, uint32_t k, uint32_t h, uint32_t q, bool active) {
   fp2_t acc;
-#if BGV_COOP_SUB == 3 && BGV_COOP_HALF == 2
+  if constexpr (HALF == 2) {
   // half 0: f_k a0 and the w^2 term; half 1: the w^3 term (same sum order)
   if (active) {
     if (h == 0) {
@@ -165,7 +165,7 @@ __device__ __forceinline__ void coop_line_round(coop_grp& g, uint32_t k, uint32_
   if (active) g.f[k] = acc;
   __syncthreads();
   return;
-#endif
+  }
   if (active) {
     COOP_PROD(&g.f[k], &g.line[0], &g.r[k]);
     acc = g.r[k];
@@ -186,13 +186,14 @@ __device__ __forceinline__ void coop_line_round(coop_grp& g, uint32_t k, uint32_
 // Miller loop of the pair held in g (T := Q, P in px/py) by lanes k = 0..5.
 // Every lane of the workgroup calls it (barriers inside); lanes outside a
 // pair, or of a skipped pair, pass active = false.
-__device__ void coop_miller(coop_grp& g, uint32_t k, uint32_t h, uint32_t q, bool active) {
+template <int SUB, int HALF>
+__device__ void coop_miller(coop_grp_t<SUB, HALF>& g, uint32_t k, uint32_t h, uint32_t q, bool active) {
   for (int b = 62; b >= 0; b--) {
     // ---- S: f <- f^2 (not on the first iteration: f = 1)
     if (b != 62) {
       fp2_t acc = fp2_zero();
       if (active) {
-#if BGV_COOP_SUB == 3 && BGV_COOP_HALF == 2
+        if constexpr (HALF == 2) {
         // half h: products 2h, 2h + 1 of lane k; (t0 + t1) + (t2 + t3)
 #pragma unroll 1
         for (int p = 2 * (int)h; p < 2 * (int)h + 2; p++) {
@@ -206,7 +207,7 @@ __device__ void coop_miller(coop_grp& g, uint32_t k, uint32_t h, uint32_t q, boo
         g.hs[k][h] = acc;
         coop_wave_sync();
         fp2_add(acc, g.hs[k][0], g.hs[k][1]);
-#else
+        } else {
 #pragma unroll 1
         for (int p = 0; p < 4; p++) {
           const sq_term e = SQ_TAB[k][p];
@@ -216,7 +217,7 @@ __device__ void coop_miller(coop_grp& g, uint32_t k, uint32_t h, uint32_t q, boo
           if (e.xi) fp2_mul_xi(t, t);
           if (e.use) fp2_add(acc, acc, t);
         }
-#endif
+        }
       }
       __syncthreads();
       if (active) g.f[k] = acc;

@@ -220,12 +220,12 @@ def test_microbench_runs(dev):
 
 
 def test_cooperative_miller_bit_identical_to_serial(monkeypatch):
-    """The cooperative Miller loop (miller_coop.h, default, 36 lanes per pair) and the
-    one-lane loop (pairing.h, BGV_MILLER=serial) produce the same Fp12 batch
-    partial, byte for byte, and the same verdicts."""
+    """The cooperative Miller loop (miller_coop.h) in its three layouts (36,
+    6 and 18 lanes per pair) and the one-lane loop (pairing.h, BGV_MILLER=serial)
+    produce the same Fp12 batch partial, byte for byte, and the same verdicts."""
     from lodestar_amd import native
     outs = {}
-    for mode in ("serial", "coop"):
+    for mode in ("serial", "coop", "6", "18"):
         monkeypatch.setenv("BGV_MILLER", mode)
         d = native.Device(0)
         try:
@@ -240,8 +240,9 @@ def test_cooperative_miller_bit_identical_to_serial(monkeypatch):
             outs[mode] = (part, ok, jr.tolist(), jr2.tolist(), bad)
         finally:
             d.close()
-    assert outs["serial"][0] == outs["coop"][0]
-    assert outs["serial"][1:4] == outs["coop"][1:4]
+    for mode in ("coop", "6", "18"):  # 36, 6 and 18 lanes per pair
+        assert outs["serial"][0] == outs[mode][0], mode
+        assert outs["serial"][1:4] == outs[mode][1:4], mode
     assert outs["coop"][2] == G.golden_arrays()[1]
     assert outs["coop"][3] == np.where(outs["coop"][4], 0, 1).tolist()
 

@@ -26,6 +26,7 @@ pytestmark = pytest.mark.gpu
 
 MODES = {
     "latency": {},
+    "coop6_jobs18": {"BGV_MILLER": "6", "BGV_JOB_LANES": "18"},
     "bulk": {"BGV_SPLIT": "0"},
     "bulk_serial_msm": {"BGV_SPLIT": "0", "BGV_MILLER": "serial", "BGV_MSM": "1", "BGV_PAIRS": "1"},
     "c4_path": {"BGV_SPLIT": "0", "BGV_MILLER": "serial", "BGV_MSM": "1", "BGV_PAIRS": "2"},

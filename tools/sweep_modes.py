@@ -26,8 +26,15 @@ MODES = {
     "coop_msm": {"BGV_MSM": "1"},
     "split1_serial": {"BGV_SPLIT": "1", "BGV_MILLER": "serial", "BGV_MSM": "0"},
     "split1_coop_msm": {"BGV_SPLIT": "1", "BGV_MILLER": "coop", "BGV_MSM": "1"},
+    "m6": {"BGV_MILLER": "6"},
+    "m18": {"BGV_MILLER": "18"},
+    "m36": {"BGV_MILLER": "36"},
+    "serial": {"BGV_MILLER": "serial"},
+    "m6_s0": {"BGV_MILLER": "6", "BGV_SPLIT": "0"},
+    "j18": {"BGV_JOB_LANES": "18"},
+    "j6": {"BGV_JOB_LANES": "6"},
 }
-KNOBS = ("BGV_SPLIT", "BGV_MILLER", "BGV_MSM", "BGV_PAIRS", "BGV_PREFOLD")
+KNOBS = ("BGV_SPLIT", "BGV_MILLER", "BGV_MSM", "BGV_PAIRS", "BGV_PREFOLD", "BGV_JOB_LANES")
 
 
 def main():
