@@ -33,8 +33,9 @@ MODES = {
     "m6_s0": {"BGV_MILLER": "6", "BGV_SPLIT": "0"},
     "j18": {"BGV_JOB_LANES": "18"},
     "j6": {"BGV_JOB_LANES": "6"},
+    "isolated": {"BGV_OVERLAP": "0", "BGV_TIMING": "1"},
 }
-KNOBS = ("BGV_SPLIT", "BGV_MILLER", "BGV_MSM", "BGV_PAIRS", "BGV_PREFOLD", "BGV_JOB_LANES")
+KNOBS = ("BGV_SPLIT", "BGV_MILLER", "BGV_MSM", "BGV_PAIRS", "BGV_PREFOLD", "BGV_JOB_LANES", "BGV_OVERLAP", "BGV_TIMING")
 
 
 def main():
@@ -80,7 +81,10 @@ def main():
                 d.verify(da, on_device=True, want_set_codes=False)
                 t.append(time.perf_counter() - t1)
             ms = float(np.median(t)) * 1e3
-            print(json.dumps({"mode": name, "sets": n, "ms": round(ms, 3), "sets_per_s": round(n / ms * 1e3, 1)}), flush=True)
+            row = {"mode": name, "sets": n, "ms": round(ms, 3), "sets_per_s": round(n / ms * 1e3, 1)}
+            if os.environ.get("BGV_TIMING") == "1":  # per-stage event times of the last call
+                row["stage_ms"] = {k: round(v, 3) for k, v in d.last_stats.as_dict(d)["stage_ms"].items() if v > 0}
+            print(json.dumps(row), flush=True)
         d.close()
 
 
