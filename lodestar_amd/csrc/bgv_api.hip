@@ -70,6 +70,7 @@ struct bgv_ctx {
   int prefold = -1;       // BGV_PREFOLD=0|1 forces the two-level job fold (A/B tests); -1 = by batch shape
   int pairs = 0;          // BGV_PAIRS=1|2 forces sets per Miller work item (A/B tests); 0 = by batch size
   int timing = -1;        // BGV_TIMING=0|1: per-stage timing events; -1 = only for batches >= 65,536 sets
+  int defer = -1;         // BGV_DEFER bits (A/B): 1 = sig_scale after hash, 2 = sig after hash, 4 = pk stream low priority
   bool timed = true;      // the last run_stages recorded per-stage events
   int run_from = 0, run_to = 0;  // stage range of the last run_stages (bgv_last_stats)
   hipStream_t st = nullptr, st_hash = nullptr, st_pk = nullptr;
@@ -177,6 +178,7 @@ int bgv_open(int device, bgv_ctx** out) {
   if (const char* o = getenv("BGV_SPLIT")) c->split = atoi(o) != 0 ? 1 : 0;
   if (const char* o = getenv("BGV_PREFOLD")) c->prefold = atoi(o) != 0 ? 1 : 0;
   if (const char* o = getenv("BGV_TIMING")) c->timing = atoi(o) != 0 ? 1 : 0;
+  if (const char* o = getenv("BGV_DEFER")) c->defer = atoi(o);
   // hash -> set-pair Miller is the critical path: its stream (and the pubkey
   // stream feeding it) get the highest priority, signature decode/scaling the
   // lowest (it only feeds the signature tree and the 1 pair per job)
@@ -185,7 +187,7 @@ int bgv_open(int device, bgv_ctx** out) {
   if (const char* p = getenv("BGV_PRIO")) if (strcmp(p, "0") == 0) prio_hi = prio_lo;
   HIPCHK(hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, prio_lo));
   HIPCHK(hipStreamCreateWithPriority(&c->st_hash, hipStreamNonBlocking, prio_hi));
-  HIPCHK(hipStreamCreateWithPriority(&c->st_pk, hipStreamNonBlocking, prio_hi));
+  HIPCHK(hipStreamCreateWithPriority(&c->st_pk, hipStreamNonBlocking, (c->defer > 0 && (c->defer & 4)) ? prio_lo : prio_hi));
   for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
   for (auto& e : c->ev_end) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipEventCreate(&c->ev_fork));
@@ -553,6 +555,7 @@ static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int fro
   // only the messages and heads the critical path (hash -> Miller -> fold ->
   // final exp); large batches keep the set-up alone on the GPU (its
   // one-workgroup scan starves under the bulk kernels)
+  const int defer = c->defer > 0 ? (c->defer & 3) : 0;
   const bool early_hash = fork && d.split && from <= ST_HASH && to > ST_HASH;
   auto launch_one = [&](int s) -> int {
     hipStream_t st = c->st;
@@ -561,6 +564,8 @@ static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int fro
       if (s == ST_PK || s == ST_PK_SCALE) st = c->st_pk;
       if (s == ST_S_TREE || s == ST_MILLER) HIPCHK(hipStreamWaitEvent(st, dep[ST_PK_SCALE], 0));
       if (s == ST_F_TREE) HIPCHK(hipStreamWaitEvent(st, dep[ST_MILLER], 0));
+      if (defer && ((s == ST_SIG_SCALE && (defer & 1)) || (s == ST_SIG && (defer & 2))))
+        HIPCHK(hipStreamWaitEvent(st, dep[ST_HASH], 0));
     }
     if (timed) HIPCHK(hipEventRecord(c->ev[s], st));
     launch_stage(st, s, d, w);
@@ -584,8 +589,11 @@ static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int fro
     HIPCHK(hipStreamWaitEvent(c->st_pk, c->ev_prep, 0));
   }
   int order[ST_COUNT], n_order = 0;
+  // deferred signature work waits on the hash's event: the hash is enqueued first
+  const bool hash_first = !early_hash && fork && defer && from <= ST_HASH && to > ST_HASH;
+  if (hash_first) order[n_order++] = ST_HASH;
   for (int s = from; s < to; s++)
-    if (!(early_hash && s == ST_HASH)) order[n_order++] = s;
+    if (!((early_hash || hash_first) && s == ST_HASH)) order[n_order++] = s;
   for (int oi = 0; oi < n_order; oi++)
     if (int r = launch_one(order[oi])) return r;
   HIPCHK(hipEventRecord(c->ev[to], c->st));

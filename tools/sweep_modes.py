@@ -34,8 +34,15 @@ MODES = {
     "j18": {"BGV_JOB_LANES": "18"},
     "j6": {"BGV_JOB_LANES": "6"},
     "isolated": {"BGV_OVERLAP": "0", "BGV_TIMING": "1"},
+    "d1": {"BGV_DEFER": "1"},
+    "d2": {"BGV_DEFER": "2"},
+    "d4": {"BGV_DEFER": "4"},
+    "d5": {"BGV_DEFER": "5"},
+    "d6": {"BGV_DEFER": "6"},
+    "noprio": {"BGV_PRIO": "0"},
 }
-KNOBS = ("BGV_SPLIT", "BGV_MILLER", "BGV_MSM", "BGV_PAIRS", "BGV_PREFOLD", "BGV_JOB_LANES", "BGV_OVERLAP", "BGV_TIMING")
+KNOBS = ("BGV_SPLIT", "BGV_MILLER", "BGV_MSM", "BGV_PAIRS", "BGV_PREFOLD", "BGV_JOB_LANES", "BGV_OVERLAP", "BGV_TIMING",
+         "BGV_DEFER", "BGV_PRIO")
 
 
 def main():
@@ -82,7 +89,7 @@ def main():
                 t.append(time.perf_counter() - t1)
             ms = float(np.median(t)) * 1e3
             row = {"mode": name, "sets": n, "ms": round(ms, 3), "sets_per_s": round(n / ms * 1e3, 1)}
-            if os.environ.get("BGV_TIMING") == "1":  # per-stage event times of the last call
+            if os.environ.get("BGV_TIMING") == "1" or n >= 65536:  # per-stage event times of the last call
                 row["stage_ms"] = {k: round(v, 3) for k, v in d.last_stats.as_dict(d)["stage_ms"].items() if v > 0}
             print(json.dumps(row), flush=True)
         d.close()
