@@ -305,51 +305,3 @@ dst = os.path.join(ROOT, "lodestar_amd", "csrc", "bls_consts.h")
 with open(dst, "w") as f:
     f.write("\n".join(out) + "\n")
 print("wrote", dst)
-
-# --------------------------------------------------------------------------
-# fd_consts.h: the signed-digit layer of the latency kernels (csrc/fd.h):
-# 14 digits of 28 bits, Montgomery R = 2^392
-# --------------------------------------------------------------------------
-RD = 1 << 392
-
-
-def digits28(v):
-    assert 0 <= v < (1 << 392)
-    return [(v >> (28 * k)) & ((1 << 28) - 1) for k in range(14)]
-
-
-def fd_lit(v, montgomery=True):
-    vv = (v % P) * RD % P if montgomery else v
-    return "{{" + ", ".join("0x%07x" % d for d in digits28(vv)) + "}}"
-
-
-def fd2_lit(c):
-    return "{" + fd_lit(c[0]) + ", " + fd_lit(c[1]) + "}"
-
-
-fo = []
-w = fo.append
-w("// GENERATED by tools/gen_constants.py from the curve definition -- do not edit.")
-w("// Signed-digit Fp of the latency kernels (fd.h): 14 x 28-bit digits, Montgomery R = 2^392.")
-w("#pragma once")
-w("")
-w("namespace bgv {")
-w("")
-w("// p in digits (plain), -p^-1 mod 2^28; p / 2^364 as a float for the fold estimate")
-w("constexpr int32_t FD_P28[14] = {" + ", ".join("0x%07x" % d for d in digits28(P)) + "};")
-w("constexpr uint32_t FD_PINV = 0x%07xu;" % ((-pow(P, -1, 1 << 28)) % (1 << 28)))
-w("constexpr float FD_INV_PTOP = %.9ef;" % (float(1 << 364) / P))
-w("// conversions: fd(x) = mont392(X, 2^400 mod p) for X = x 2^384 (fp_t); fp(x) = mont392(Y, 2^384 mod p)")
-w("BGV_CONST fd_t FD_C_IN = " + fd_lit(pow(2, 400, P), False) + ";")
-w("BGV_CONST fd_t FD_C_OUT = " + fd_lit(pow(2, 384, P), False) + ";")
-w("BGV_CONST fd_t FD_ONE = " + fd_lit(1) + ";")
-w("BGV_CONST fd2_t FD_PSI_CX = " + fd2_lit(PSI_CX) + ";")
-w("BGV_CONST fd2_t FD_PSI_CY = " + fd2_lit(PSI_CY) + ";")
-w("BGV_CONST fd_t FD_PSI2_CX = " + fd_lit(psi2x[0]) + ";")
-w("BGV_CONST fd_t FD_PSI2_CY = " + fd_lit(psi2y[0]) + ";")
-w("")
-w("}  // namespace bgv")
-dst = os.path.join(ROOT, "lodestar_amd", "csrc", "fd_consts.h")
-with open(dst, "w") as f:
-    f.write("\n".join(fo) + "\n")
-print("wrote", dst)
