@@ -219,12 +219,24 @@ template <class F> BGV_NI void jac_mul_u64_w4(jac_t<F>& r, const jac_t<F>& p, ui
   r = acc;
 }
 
-// [|x|]P for the BLS parameter (Hamming weight 6)
+// the addition as a call (one copy per unit): the x-chain and the cofactor
+// map below keep only their doubling inlined, so its temporaries stay in
+// registers instead of sharing a frame with the addition's
+template <class F> BGV_NI void jac_add_call(jac_t<F>& r, const jac_t<F>& p, const jac_t<F>& q) { jac_add(r, p, q); }
+
+// [|x|]P for the BLS parameter: |x| = 0xd201000000010000 has its bits 63,
+// 62, 60, 57, 48 and 16 set, so after the top bit the double-and-add is runs
+// of 1, 2, 3, 9, 32 doublings, each followed by an addition, then 16
+// doublings (the same operations as the bitwise loop, in the same order)
 template <class F> BGV_NIC void jac_mul_abs_x(jac_t<F>& r, const jac_t<F>& p) {
+  static_assert(BLS_X_ABS_C == 0xd201000000010000ull, "x-chain runs");
   jac_t<F> acc = p;
-  for (int b = 62; b >= 0; b--) {
-    jac_dbl(acc, acc);
-    if ((BLS_X_ABS >> b) & 1ull) jac_add(acc, acc, p);
+#pragma unroll 1
+  for (int s = 0; s < 6; s++) {
+    const int run = s == 0 ? 1 : (s == 1 ? 2 : (s == 2 ? 3 : (s == 3 ? 9 : (s == 4 ? 32 : 16))));
+#pragma unroll 1
+    for (int k = 0; k < run; k++) jac_dbl(acc, acc);
+    if (s < 5) jac_add_call(acc, acc, p);
   }
   r = acc;
 }
@@ -308,15 +320,15 @@ BGV_NIC void g2_clear_cofactor(g2j& r, const g2j& p) {
   jac_mul_abs_x(t2, t1);
   jac_neg(t2, t2);            // [x^2]P
   jac_neg(np, p);
-  jac_add(t3, t1, np);        // [x - 1]P
+  jac_add_call(t3, t1, np);        // [x - 1]P
   g2_psi(t3, t3);             // psi([x-1]P)
   jac_neg(t1, t1);
-  jac_add(t2, t2, t1);        // [x^2 - x]P
-  jac_add(t2, t2, np);        // [x^2 - x - 1]P
-  jac_add(t2, t2, t3);
+  jac_add_call(t2, t2, t1);        // [x^2 - x]P
+  jac_add_call(t2, t2, np);        // [x^2 - x - 1]P
+  jac_add_call(t2, t2, t3);
   jac_dbl(t1, p);
   g2_psi2(t1, t1);
-  jac_add(r, t2, t1);
+  jac_add_call(r, t2, t1);
 }
 
 // ---- serialization ---------------------------------------------------------

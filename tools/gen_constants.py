@@ -240,6 +240,7 @@ w("BGV_CONST fp_t P_HALF = " + fp_lit((P - 1) // 2, False) + ";")
 w("")
 w("// |x| of the BLS parameter x = -0xd201000000010000")
 w("BGV_CONST uint64_t BLS_X_ABS = 0x%016xull;" % (-X_PARAM))
+w("constexpr uint64_t BLS_X_ABS_C = 0x%016xull;  // compile-time copy (curve.h x-chain runs)" % (-X_PARAM))
 w("")
 w("// E1: y^2 = x^3 + 4 ; E2: y^2 = x^3 + 4(1+i)")
 w("BGV_CONST fp_t B1_MONT = " + fp_lit(4) + ";")
