@@ -245,6 +245,16 @@ int bgv_gen_keys(bgv_ctx* ctx, uint32_t first_index, uint32_t n, uint64_t seed);
  * Pointers follow batch->on_device; sigs_out is in the same space. */
 int bgv_gen_sign(bgv_ctx* ctx, const bgv_batch* batch, uint8_t* sigs_out192);
 
+/* ---- field self-test (tests only) ---------------------------------------- */
+/* The device's modular add/sub primitives on n operand pairs: ab_in holds
+ * a_i || b_i as 2 x 12 little-endian u32 limbs (each < p; add and sub mod p
+ * are independent of the Montgomery form), out receives BGV_FP_OPS_N
+ * elements of 12 limbs per pair: a+b, a-b, [a+b, 2b] (dual add), [a-b, b-a]
+ * (dual sub), [a+b, a-b] (add/sub pair), [a+b, 2a] unreduced (dual lazy
+ * add), -a.  Host pointers. */
+#define BGV_FP_OPS_N 11
+int bgv_debug_fp_ops(bgv_ctx* ctx, const uint32_t* ab_in, uint32_t n, uint32_t* out);
+
 /* ---- microbenchmarks for the roofline ------------------------ */
 /* Montgomery Fp-mul throughput: `lanes` independent chains of `iters`
  * products; returns device ms (HIP events). */

@@ -863,6 +863,23 @@ int bgv_gen_sign(bgv_ctx* c, const bgv_batch* b, uint8_t* sigs_out) {
   return BGV_OK;
 }
 
+// ---- field self-test ---------------------------------------------------------
+int bgv_debug_fp_ops(bgv_ctx* c, const uint32_t* ab_in, uint32_t n, uint32_t* out) {
+  if (!c || (n && (!ab_in || !out))) return fail(BGV_E_INVALID_ARG, "null argument");
+  if (n > (1u << 20)) return fail(BGV_E_INVALID_ARG, "at most 2^20 operand pairs");
+  if (!n) return BGV_OK;
+  HIPCHK(hipSetDevice(c->device));
+  if (int r = c->mb_fp.ensure((size_t)n * (2 + BGV_FP_OPS_N))) return r;
+  fp_t* d_ab = c->mb_fp.p;
+  fp_t* d_out = d_ab + (size_t)n * 2;
+  HIPCHK(hipMemcpyAsync(d_ab, ab_in, (size_t)n * 2 * sizeof(fp_t), hipMemcpyHostToDevice, c->st));
+  launch_fp_ops(c->st, d_ab, d_out, n);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, d_out, (size_t)n * BGV_FP_OPS_N * sizeof(fp_t), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return BGV_OK;
+}
+
 // ---- microbenchmarks ---------------------------------------------------------
 int bgv_bench_fpmul(bgv_ctx* c, uint32_t lanes, uint32_t iters, float* ms) {
   if (!c || !ms || lanes == 0 || lanes % 256) return fail(BGV_E_INVALID_ARG, "lanes must be a positive multiple of 256");

@@ -105,6 +105,7 @@ void launch_export_g2a(hipStream_t st, const g2a* in, uint8_t* out192, uint32_t 
 void launch_fp12_convert(hipStream_t st, const fp12_t* in, fp12_t* out, uint32_t n, bool to_mont);
 void launch_gen_keys(hipStream_t st, g1a* table, uint32_t* sk, uint32_t first, uint32_t n, uint64_t seed);
 void launch_gen_sign(hipStream_t st, const dev_batch& b, const uint32_t* sk, uint8_t* out);
+void launch_fp_ops(hipStream_t st, const fp_t* ab, fp_t* out, uint32_t n);
 void launch_bench_fpmul(hipStream_t st, fp_t* io, uint32_t lanes, uint32_t iters);
 void launch_gen_scalars(hipStream_t st, const uint32_t key[8], const uint32_t nonce[3], uint64_t* out, uint32_t n);
 void launch_bench_mad(hipStream_t st, uint64_t* io, uint32_t lanes, uint32_t iters);

@@ -842,6 +842,26 @@ __global__ void BGV_BULK k_gen_sign(dev_batch b, const uint32_t* sk_store, uint8
   g2_compress(sigs_out + 192u * i, sig);
 }
 
+// ===================================================== field self-test
+// bgv_debug_fp_ops: the device's modular additions (the inline-asm chains of
+// fp_asm.h and their single / dual / lazy forms) on host-chosen operands,
+// limbs in and out as they are (add and sub mod p do not care about the
+// Montgomery form).  out[FP_OPS_N * i + k], k as in include/bgv.h.
+__global__ void BGV_BULK k_fp_ops(const fp_t* ab, fp_t* out, uint32_t n) {
+  const uint32_t i = gtid();
+  if (i >= n) return;
+  const fp_t a = ab[2 * i], b = ab[2 * i + 1];
+  fp_t* o = out + 11u * i;
+  fp_t r0, r1;
+  fp_add(r0, a, b); o[0] = r0;
+  fp_sub(r0, a, b); o[1] = r0;
+  fp_add2(r0, a, b, r1, b, b); o[2] = r0; o[3] = r1;
+  fp_sub2(r0, a, b, r1, b, a); o[4] = r0; o[5] = r1;
+  fp_add_sub(r0, a, b, r1, a, b); o[6] = r0; o[7] = r1;
+  fp_add_lazy2(r0, a, b, r1, a, a); o[8] = r0; o[9] = r1;
+  fp_neg(r0, a); o[10] = r0;
+}
+
 // ========================================================= microbenchmarks
 __global__ void __launch_bounds__(256) k_bench_fpmul(fp_t* io, uint32_t iters) {
   const uint32_t i = gtid();
@@ -1017,6 +1037,9 @@ void launch_gen_keys(hipStream_t st, g1a* table, uint32_t* sk, uint32_t first, u
 }
 void launch_gen_sign(hipStream_t st, const dev_batch& b, const uint32_t* sk, uint8_t* out) {
   BGV_LAUNCH(k_gen_sign, b.n_sets, b, sk, out);
+}
+void launch_fp_ops(hipStream_t st, const fp_t* ab, fp_t* out, uint32_t n) {
+  if (n) hipLaunchKernelGGL(k_fp_ops, dim3((n + 63u) / 64u), dim3(64), 0, st, ab, out, n);
 }
 void launch_bench_fpmul(hipStream_t st, fp_t* io, uint32_t lanes, uint32_t iters) {
   hipLaunchKernelGGL(k_bench_fpmul, dim3(lanes / 256), dim3(256), 0, st, io, iters);

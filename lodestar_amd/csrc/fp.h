@@ -91,7 +91,23 @@ BGV_HD void fp_reduce_once(fp_t& r, const fp_t& a) {
   for (int i = 0; i < NL; i++) r.l[i] = (a.l[i] & m) | (t[i] & ~m);
 }
 
+#ifndef BGV_ASM_ADD
+#define BGV_ASM_ADD 1  // device: interleaved-chain inline asm (fp_asm.h)
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && BGV_ASM_ADD
+#define BGV_ASM_ON 1
+#else
+#define BGV_ASM_ON 0
+#endif
+}  // namespace bgv
+#include "fp_asm.h"
+namespace bgv {
+
 BGV_HD void fp_add(fp_t& r, const fp_t& a, const fp_t& b) {
+#if BGV_ASM_ON
+  fpa_add(r, a, b);
+  return;
+#endif
   fp_t s;
   uint32_t carry = 0;
 #pragma unroll
@@ -119,6 +135,10 @@ BGV_HD void fp_add_lazy(fp_t& r, const fp_t& a, const fp_t& b) {
 }
 
 BGV_HD void fp_sub(fp_t& r, const fp_t& a, const fp_t& b) {
+#if BGV_ASM_ON
+  fpa_sub(r, a, b);
+  return;
+#endif
   uint32_t t[NL];
   uint32_t borrow = 0;
 #pragma unroll

@@ -16,25 +16,62 @@ BGV_HD void fp2_select(fp2_t& r, bool c, const fp2_t& a, const fp2_t& b) {
   fp_select(r.c1, c, a.c1, b.c1);
 }
 
-BGV_HD void fp2_add(fp2_t& r, const fp2_t& a, const fp2_t& b) { fp_add(r.c0, a.c0, b.c0); fp_add(r.c1, a.c1, b.c1); }
-BGV_HD void fp2_sub(fp2_t& r, const fp2_t& a, const fp2_t& b) { fp_sub(r.c0, a.c0, b.c0); fp_sub(r.c1, a.c1, b.c1); }
-BGV_HD void fp2_dbl(fp2_t& r, const fp2_t& a) { fp_dbl(r.c0, a.c0); fp_dbl(r.c1, a.c1); }
-BGV_HD void fp2_neg(fp2_t& r, const fp2_t& a) { fp_neg(r.c0, a.c0); fp_neg(r.c1, a.c1); }
+// two independent modular operations at once (one asm block, interleaved
+// carry chains on the device; fp_asm.h)
+BGV_HD void fp_add2(fp_t& r0, const fp_t& a0, const fp_t& b0, fp_t& r1, const fp_t& a1, const fp_t& b1) {
+#if BGV_ASM_ON
+  fpa_add_add(r0, a0, b0, r1, a1, b1);
+#else
+  fp_add(r0, a0, b0);
+  fp_add(r1, a1, b1);
+#endif
+}
+BGV_HD void fp_sub2(fp_t& r0, const fp_t& a0, const fp_t& b0, fp_t& r1, const fp_t& a1, const fp_t& b1) {
+#if BGV_ASM_ON
+  fpa_sub_sub(r0, a0, b0, r1, a1, b1);
+#else
+  fp_sub(r0, a0, b0);
+  fp_sub(r1, a1, b1);
+#endif
+}
+// r0 = a0 + b0, r1 = a1 - b1
+BGV_HD void fp_add_sub(fp_t& r0, const fp_t& a0, const fp_t& b0, fp_t& r1, const fp_t& a1, const fp_t& b1) {
+#if BGV_ASM_ON
+  fpa_add_sub(r0, a0, b0, r1, a1, b1);
+#else
+  fp_add(r0, a0, b0);
+  fp_sub(r1, a1, b1);
+#endif
+}
+BGV_HD void fp_add_lazy2(fp_t& r0, const fp_t& a0, const fp_t& b0, fp_t& r1, const fp_t& a1, const fp_t& b1) {
+#if BGV_ASM_ON && BGV_FPMUL28_LAZY
+  fpa_addnr_addnr(r0, a0, b0, r1, a1, b1);
+#else
+  fp_add_lazy(r0, a0, b0);
+  fp_add_lazy(r1, a1, b1);
+#endif
+}
+
+BGV_HD void fp2_add(fp2_t& r, const fp2_t& a, const fp2_t& b) { fp_add2(r.c0, a.c0, b.c0, r.c1, a.c1, b.c1); }
+BGV_HD void fp2_sub(fp2_t& r, const fp2_t& a, const fp2_t& b) { fp_sub2(r.c0, a.c0, b.c0, r.c1, a.c1, b.c1); }
+BGV_HD void fp2_dbl(fp2_t& r, const fp2_t& a) { fp_add2(r.c0, a.c0, a.c0, r.c1, a.c1, a.c1); }
+BGV_HD void fp2_neg(fp2_t& r, const fp2_t& a) {
+  const fp_t z = fp_zero();
+  fp_sub2(r.c0, z, a.c0, r.c1, z, a.c1);
+}
 BGV_HD void fp2_conj(fp2_t& r, const fp2_t& a) { r.c0 = a.c0; fp_neg(r.c1, a.c1); }
-BGV_HD void fp2_mul3(fp2_t& r, const fp2_t& a) { fp_mul3(r.c0, a.c0); fp_mul3(r.c1, a.c1); }
-BGV_HD void fp2_mul4(fp2_t& r, const fp2_t& a) { fp_mul4(r.c0, a.c0); fp_mul4(r.c1, a.c1); }
-BGV_HD void fp2_mul8(fp2_t& r, const fp2_t& a) { fp_mul8(r.c0, a.c0); fp_mul8(r.c1, a.c1); }
+BGV_HD void fp2_mul3(fp2_t& r, const fp2_t& a) { fp2_t t; fp2_dbl(t, a); fp2_add(r, t, a); }
+BGV_HD void fp2_mul4(fp2_t& r, const fp2_t& a) { fp2_t t; fp2_dbl(t, a); fp2_dbl(r, t); }
+BGV_HD void fp2_mul8(fp2_t& r, const fp2_t& a) { fp2_t t; fp2_dbl(t, a); fp2_dbl(t, t); fp2_dbl(r, t); }
 
 // Karatsuba: 3 Fp products
 BGV_NI2 void fp2_mul(fp2_t& r, const fp2_t& a, const fp2_t& b) {
   fp_t t0, t1, t2, t3;
   fp_mul(t0, a.c0, b.c0);
   fp_mul(t1, a.c1, b.c1);
-  fp_add_lazy(t2, a.c0, a.c1);  // < 2p, product inputs only
-  fp_add_lazy(t3, b.c0, b.c1);
+  fp_add_lazy2(t2, a.c0, a.c1, t3, b.c0, b.c1);  // < 2p, product inputs only
   fp_mul(t2, t2, t3);
-  fp_sub(r.c0, t0, t1);
-  fp_sub(t2, t2, t0);
+  fp_sub2(r.c0, t0, t1, t2, t2, t0);
   fp_sub(r.c1, t2, t1);
 }
 
@@ -44,11 +81,9 @@ BGV_HD void fp2_mul_inl(fp2_t& r, const fp2_t& a, const fp2_t& b) {
   fp_t t0, t1, t2, t3;
   fp_mul(t0, a.c0, b.c0);
   fp_mul(t1, a.c1, b.c1);
-  fp_add_lazy(t2, a.c0, a.c1);  // < 2p, product inputs only
-  fp_add_lazy(t3, b.c0, b.c1);
+  fp_add_lazy2(t2, a.c0, a.c1, t3, b.c0, b.c1);  // < 2p, product inputs only
   fp_mul(t2, t2, t3);
-  fp_sub(r.c0, t0, t1);
-  fp_sub(t2, t2, t0);
+  fp_sub2(r.c0, t0, t1, t2, t2, t0);
   fp_sub(r.c1, t2, t1);
 }
 
@@ -67,8 +102,7 @@ BGV_NI2 void fp2_mul_fp(fp2_t& r, const fp2_t& a, const fp_t& b) { fp_mul(r.c0, 
 // multiply by the tower non-residue xi = 1 + i
 BGV_HD void fp2_mul_xi(fp2_t& r, const fp2_t& a) {
   fp_t t0, t1;
-  fp_sub(t0, a.c0, a.c1);
-  fp_add(t1, a.c0, a.c1);
+  fp_add_sub(t1, a.c0, a.c1, t0, a.c0, a.c1);
   r.c0 = t0;
   r.c1 = t1;
 }

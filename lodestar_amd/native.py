@@ -49,8 +49,9 @@ EXPORTS = [
     "bgv_abi_version", "bgv_set_code_name", "bgv_stage_name", "bgv_last_error", "bgv_open", "bgv_close",
     "bgv_pubkeys_set", "bgv_pubkeys_count", "bgv_pubkeys_get", "bgv_pubkeys_validate", "bgv_verify", "bgv_last_stats",
     "bgv_partial", "bgv_partial_finish", "bgv_combine_final", "bgv_debug_stages", "bgv_gen_keys", "bgv_gen_sign", "bgv_bench_fpmul",
-    "bgv_bench_mad",
+    "bgv_bench_mad", "bgv_debug_fp_ops",
 ]
+FP_OPS_N = 11
 
 
 class BgvNativeError(RuntimeError):
@@ -142,6 +143,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
             "bgv_gen_sign": ([P, ctypes.POINTER(BgvBatch), P], ctypes.c_int),
             "bgv_bench_fpmul": ([P, u32, u32, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
             "bgv_bench_mad": ([P, u32, u32, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+            "bgv_debug_fp_ops": ([P, P, u32, P], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(lib, name)
@@ -296,6 +298,15 @@ class Device:
     def gen_sign(self, arrays: dict, out, on_device: bool = False):
         b = self.make_batch(arrays, on_device)
         self._check(self.lib.bgv_gen_sign(self.h, ctypes.byref(b), _ptr(out)))
+
+    def debug_fp_ops(self, ab: np.ndarray) -> np.ndarray:
+        """Device modular add/sub primitives (test only): ab is (n, 2, 12) u32
+        limbs; returns (n, FP_OPS_N, 12) u32 (include/bgv.h bgv_debug_fp_ops)."""
+        ab = np.ascontiguousarray(ab, dtype=np.uint32)
+        n = ab.shape[0]
+        out = np.zeros((n, FP_OPS_N, 12), np.uint32)
+        self._check(self.lib.bgv_debug_fp_ops(self.h, ab.ctypes.data, n, out.ctypes.data))
+        return out
 
     # ---------------------------------------------------------- microbench
     def bench_fpmul(self, lanes: int, iters: int) -> float:
