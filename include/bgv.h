@@ -251,8 +251,8 @@ int bgv_gen_sign(bgv_ctx* ctx, const bgv_batch* batch, uint8_t* sigs_out192);
  * are independent of the Montgomery form), out receives BGV_FP_OPS_N
  * elements of 12 limbs per pair: a+b, a-b, [a+b, 2b] (dual add), [a-b, b-a]
  * (dual sub), [a+b, a-b] (add/sub pair), [a+b, 2a] unreduced (dual lazy
- * add), -a.  Host pointers. */
-#define BGV_FP_OPS_N 11
+ * add), -a, [a+b unreduced, b-a] (lazy add / sub pair).  Host pointers. */
+#define BGV_FP_OPS_N 13
 int bgv_debug_fp_ops(bgv_ctx* ctx, const uint32_t* ab_in, uint32_t n, uint32_t* out);
 
 /* ---- microbenchmarks for the roofline ------------------------ */

@@ -851,7 +851,7 @@ __global__ void BGV_BULK k_fp_ops(const fp_t* ab, fp_t* out, uint32_t n) {
   const uint32_t i = gtid();
   if (i >= n) return;
   const fp_t a = ab[2 * i], b = ab[2 * i + 1];
-  fp_t* o = out + 11u * i;
+  fp_t* o = out + 13u * i;
   fp_t r0, r1;
   fp_add(r0, a, b); o[0] = r0;
   fp_sub(r0, a, b); o[1] = r0;
@@ -860,6 +860,7 @@ __global__ void BGV_BULK k_fp_ops(const fp_t* ab, fp_t* out, uint32_t n) {
   fp_add_sub(r0, a, b, r1, a, b); o[6] = r0; o[7] = r1;
   fp_add_lazy2(r0, a, b, r1, a, a); o[8] = r0; o[9] = r1;
   fp_neg(r0, a); o[10] = r0;
+  fp_addnr_sub(r0, a, b, r1, b, a); o[11] = r0; o[12] = r1;
 }
 
 // ========================================================= microbenchmarks

@@ -45,8 +45,7 @@ __device__ __forceinline__ fp2_t cg_sel(uint32_t s, const fp2_t& x0, const fp2_t
 
 __device__ __forceinline__ void cg_combine(fp2_t& o, const fp_t* P) {
   fp_t w;
-  fp_sub(o.c0, P[0], P[1]);
-  fp_add(w, P[0], P[1]);
+  fp_add_sub(w, P[0], P[1], o.c0, P[0], P[1]);
   fp_sub(o.c1, P[2], w);
 }
 
@@ -77,15 +76,12 @@ BGV_CGF void cg_round(cg_scratch* S, uint32_t s, uint32_t q, int n, const fp2_t&
   // then every lane reads the n products back: one more LDS exchange
   // instead of 3 x 3 redundant additions on every lane
   if ((int)s < n && q < 2) {
+    // both lanes run the same dual add/sub (no divergent branches), then
+    // lane 1 finishes c1 = P2 - (P0 + P1)
     const fp_t p0 = lds_get(&L->P[s][0]), p1 = lds_get(&L->P[s][1]);
-    fp_t o;
-    if (q == 0) {
-      fp_sub(o, p0, p1);
-    } else {
-      fp_t w;
-      fp_add(w, p0, p1);
-      fp_sub(o, lds_get(&L->P[s][2]), w);
-    }
+    fp_t o, w;
+    fp_add_sub(w, p0, p1, o, p0, p1);
+    if (q == 1) fp_sub(o, lds_get(&L->P[s][2]), w);
     lds_put(&L->O[s][q], o);
   }
   coop_wave_sync();

@@ -63,8 +63,7 @@ __device__ void c_mul(wfp12* out_, const wfp12* a_, const wfp12* b_, cscratch* s
     const fp_t p0 = lds_get(&s->p[3 * l]), p1 = lds_get(&s->p[3 * l + 1]), p2 = lds_get(&s->p[3 * l + 2]);
     fp2_t t;
     fp_t w;
-    fp_sub(t.c0, p0, p1);
-    fp_add(w, p0, p1);
+    fp_add_sub(w, p0, p1, t.c0, p0, p1);
     fp_sub(t.c1, p2, w);
     if (i + j >= 6) fp2_mul_xi(t, t);
     lds_put(&s->q[l].c0, t.c0);
@@ -73,12 +72,17 @@ __device__ void c_mul(wfp12* out_, const wfp12* a_, const wfp12* b_, cscratch* s
   __syncthreads();
   if (l < 12) {
     const uint32_t k = l >> 1, comp = l & 1;
-    fp_t acc = lds_get(comp ? &s->q[k].c1 : &s->q[k].c0);  // i = 0, j = k
+    // c_k = sum_i q[i][k - i]: a tree of dual additions, ((t0 + t1) + (t2 + t3)) + (t4 + t5)
+    fp_t t[6];
 #pragma unroll
-    for (uint32_t i = 1; i < 6; i++) {
-      const BGV_LDS fp2_t* t = &s->q[i * 6 + (k + 6 - i) % 6];
-      fp_add(acc, acc, lds_get(comp ? &t->c1 : &t->c0));
+    for (uint32_t i = 0; i < 6; i++) {
+      const BGV_LDS fp2_t* e = &s->q[i * 6 + (k + 6 - i) % 6];
+      t[i] = lds_get(comp ? &e->c1 : &e->c0);
     }
+    fp_t s01, s23, s45, acc;
+    fp_add2(s01, t[0], t[1], s23, t[2], t[3]);
+    fp_add2(s45, t[4], t[5], acc, s01, s23);
+    fp_add(acc, acc, s45);
     lds_put(comp ? &out->c[k].c1 : &out->c[k].c0, acc);
   }
   __syncthreads();

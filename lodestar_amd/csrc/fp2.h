@@ -43,6 +43,15 @@ BGV_HD void fp_add_sub(fp_t& r0, const fp_t& a0, const fp_t& b0, fp_t& r1, const
   fp_sub(r1, a1, b1);
 #endif
 }
+// r0 = a0 + b0 unreduced (< 2p, product input only), r1 = a1 - b1 mod p
+BGV_HD void fp_addnr_sub(fp_t& r0, const fp_t& a0, const fp_t& b0, fp_t& r1, const fp_t& a1, const fp_t& b1) {
+#if BGV_ASM_ON && BGV_FPMUL28_LAZY
+  fpa_addnr_sub(r0, a0, b0, r1, a1, b1);
+#else
+  fp_add_lazy(r0, a0, b0);
+  fp_sub(r1, a1, b1);
+#endif
+}
 BGV_HD void fp_add_lazy2(fp_t& r0, const fp_t& a0, const fp_t& b0, fp_t& r1, const fp_t& a1, const fp_t& b1) {
 #if BGV_ASM_ON && BGV_FPMUL28_LAZY
   fpa_addnr_addnr(r0, a0, b0, r1, a1, b1);
@@ -90,8 +99,7 @@ BGV_HD void fp2_mul_inl(fp2_t& r, const fp2_t& a, const fp2_t& b) {
 // complex squaring: 2 Fp products
 BGV_NI2 void fp2_sqr(fp2_t& r, const fp2_t& a) {
   fp_t t0, t1, t2;
-  fp_add_lazy(t0, a.c0, a.c1);  // < 2p, product input only
-  fp_sub(t1, a.c0, a.c1);
+  fp_addnr_sub(t0, a.c0, a.c1, t1, a.c0, a.c1);  // t0 < 2p, product input only
   fp_mul(t2, a.c0, a.c1);
   fp_mul(r.c0, t0, t1);
   fp_dbl(r.c1, t2);

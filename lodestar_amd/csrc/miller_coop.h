@@ -116,15 +116,12 @@ __device__ __forceinline__ void coop_prod_sub(fp_t* P, uint32_t q, const fp2_t* 
   fp_mul(r, u, v);
   P[q] = r;
   coop_wave_sync();
-  if (q == 0) {
-    fp_t t;
-    fp_sub(t, P[0], P[1]);
-    out->c0 = t;
-  } else if (q == 1) {
+  if (q < 2) {  // one dual add/sub on both lanes (no divergent branches), lane 1 finishes c1
     fp_t t, w;
-    fp_add(w, P[0], P[1]);
-    fp_sub(t, P[2], w);
-    out->c1 = t;
+    fp_add_sub(w, P[0], P[1], t, P[0], P[1]);
+    if (q == 1) fp_sub(t, P[2], w);
+    if (q == 0) out->c0 = t;
+    else out->c1 = t;
   }
   coop_wave_sync();
 }

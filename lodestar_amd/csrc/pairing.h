@@ -13,6 +13,14 @@
 #else
 #define BGV_NIS BGV_NI
 #endif
+// the two-pair loop inlined into its kernel (BGV_LOOP2_INLINE): a __shared__
+// accumulator is then seen as LDS by every inlined helper (ds_read/ds_write
+// instead of flat accesses)
+#if defined(__HIPCC__) && BGV_LOOP2_INLINE
+#define BGV_NIL BGV_HD
+#else
+#define BGV_NIL BGV_NI
+#endif
 
 namespace bgv {
 
@@ -129,7 +137,7 @@ BGV_NI void miller_loop(fp12_t& f, const g1a& P, bool p_inf, const g2a& Q, bool 
 // Two pairs with ONE shared accumulator: f = f_{x,Q1}(P1) * f_{x,Q2}(P2),
 // so the Fp12 squaring of every iteration is paid once for both pairs
 // (the multi-Miller loop of blst's miller_loop_n, at width 2).
-BGV_NI void miller_loop2(fp12_t& f, const g1a& P1, const g2a& Q1, const g1a& P2, const g2a& Q2) {
+BGV_NIL void miller_loop2(fp12_t& f, const g1a& P1, const g2a& Q1, const g1a& P2, const g2a& Q2) {
   g2p_t T1, T2;
   T1.x = Q1.x; T1.y = Q1.y; T1.z = fp2_one();
   T2.x = Q2.x; T2.y = Q2.y; T2.z = fp2_one();

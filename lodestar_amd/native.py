@@ -51,7 +51,7 @@ EXPORTS = [
     "bgv_partial", "bgv_partial_finish", "bgv_combine_final", "bgv_debug_stages", "bgv_gen_keys", "bgv_gen_sign", "bgv_bench_fpmul",
     "bgv_bench_mad", "bgv_debug_fp_ops",
 ]
-FP_OPS_N = 11
+FP_OPS_N = 13
 
 
 class BgvNativeError(RuntimeError):

@@ -186,7 +186,7 @@ def main():
     parts = [HEADER]
     names = {"add": "add", "sub": "sub", "lazy": "addnr"}
     for ops in [("add",), ("sub",), ("add", "add"), ("sub", "sub"), ("add", "sub"), ("lazy", "lazy"),
-                ("add", "add", "add"), ("sub", "sub", "sub")]:
+                ("lazy", "sub"), ("add", "add", "add"), ("sub", "sub", "sub")]:
         name = "fpa_" + "_".join(names[o] for o in ops)
         doc = "; ".join(f"r{k} = a{k} {'+' if o != 'sub' else '-'} b{k}{'' if o == 'lazy' else ' mod p'}"
                         for k, o in enumerate(ops))
