@@ -6,7 +6,11 @@
 // job for its (-G1, S_job) pair.  Item offsets per job come from a scan
 // (bgv_kernels.hip k_item_count / k_item_job).
 #ifndef BGV_FPMUL_CALL
+#ifdef BGV_MILLER_FPMUL_CALL
+#define BGV_FPMUL_CALL BGV_MILLER_FPMUL_CALL
+#else
 #define BGV_FPMUL_CALL 1
+#endif
 #endif
 #ifndef BGV_FP2_INLINE
 #define BGV_FP2_INLINE 1
