@@ -71,6 +71,7 @@ struct bgv_ctx {
   int pairs = 0;          // BGV_PAIRS=1|2 forces sets per Miller work item (A/B tests); 0 = by batch size
   int timing = -1;        // BGV_TIMING=0|1: per-stage timing events; -1 = only for batches >= 65,536 sets
   int defer = -1;         // BGV_DEFER bits (A/B): 1 = sig_scale after hash, 2 = sig after hash, 4 = pk stream low priority
+  int defer_grp = -1;     // BGV_DEFER_GRP=0|1: bulk-mode subgroup checks beside the Miller loops; -1 = on
   bool timed = true;      // the last run_stages recorded per-stage events
   int run_from = 0, run_to = 0;  // stage range of the last run_stages (bgv_last_stats)
   hipStream_t st = nullptr, st_hash = nullptr, st_pk = nullptr;
@@ -78,6 +79,8 @@ struct bgv_ctx {
   hipEvent_t ev_end[ST_COUNT] = {};   // end of stage s on its stream
   hipEvent_t ev_fork = nullptr;
   hipEvent_t ev_prep = nullptr;       // end of launch_prep (latency batches fork the hash leg before it)
+  hipEvent_t ev_sigdec = nullptr;     // defer_grp: signatures decoded (the checks may start)
+  hipEvent_t ev_grp = nullptr;        // defer_grp: subgroup checks done (the code fix-up may start)
   hipEvent_t ev_dep[ST_COUNT] = {};   // untimed cross-stream dependencies (latency batches)
   // index2pubkey table (grown by copy) and synthetic secret keys
   g1a* table = nullptr;
@@ -179,6 +182,7 @@ int bgv_open(int device, bgv_ctx** out) {
   if (const char* o = getenv("BGV_PREFOLD")) c->prefold = atoi(o) != 0 ? 1 : 0;
   if (const char* o = getenv("BGV_TIMING")) c->timing = atoi(o) != 0 ? 1 : 0;
   if (const char* o = getenv("BGV_DEFER")) c->defer = atoi(o);
+  if (const char* o = getenv("BGV_DEFER_GRP")) c->defer_grp = atoi(o) != 0 ? 1 : 0;
   // hash -> set-pair Miller is the critical path: its stream (and the pubkey
   // stream feeding it) get the highest priority, signature decode/scaling the
   // lowest (it only feeds the signature tree and the 1 pair per job)
@@ -194,6 +198,8 @@ int bgv_open(int device, bgv_ctx** out) {
   HIPCHK(hipEventCreateWithFlags(&c->ev_staged, hipEventDisableTiming));
   for (auto& e : c->ev_dep) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&c->ev_prep, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&c->ev_sigdec, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&c->ev_grp, hipEventDisableTiming));
   *out = c;
   return BGV_OK;
 }
@@ -210,6 +216,8 @@ int bgv_close(bgv_ctx* c) {
   (void)hipEventDestroy(c->ev_staged);
   for (auto& e : c->ev_dep) (void)hipEventDestroy(e);
   (void)hipEventDestroy(c->ev_prep);
+  (void)hipEventDestroy(c->ev_sigdec);
+  (void)hipEventDestroy(c->ev_grp);
   if (c->pin_in) (void)hipHostFree(c->pin_in);
   if (c->pin_out) (void)hipHostFree(c->pin_out);
   if (c->table) (void)hipFree(c->table);
@@ -466,6 +474,12 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   d.pairs_per_item = n >= PAIRS2_MIN ? 2 : 1;
   if (c->pairs == 1 || c->pairs == 2) d.pairs_per_item = (uint32_t)c->pairs;
   d.split = c->split >= 0 ? (uint32_t)c->split : (n < SPLIT_MAX ? 1u : 0u);
+  // bulk mode: decode in phase 1, subgroup checks beside the Miller loops
+  // (bgv_kernels.hip k_job_recode); the latency mode has its own split
+  // (one pair per Miller item: C4/2 28.3 -> 26.4 ms; with two pairs per item
+  // the checks slow the longer Miller phase more than they save: C4 40.4 -> 41.9)
+  d.defer_grp = c->defer_grp >= 0 ? (uint32_t)(!d.split && c->defer_grp)
+                                  : ((!d.split && d.pairs_per_item == 1) ? 1u : 0u);
   // two-level per-job fold (bgv_tail.hip) when few jobs of >= 64 sets leave
   // the chip idle: groups of ~sqrt(span) sets fold side by side, then the job
   // folds the group values, 2 sqrt(span) sequential Fp12 products instead of span
@@ -522,6 +536,9 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
   if (d.split) {
     if ((r = c->q_part.ensure(2 * ns)) || (r = c->sig_grp.ensure(ns))) return r;
     w.q_part = c->q_part.p; w.sig_grp = c->sig_grp.p;
+  } else if (d.defer_grp) {
+    if ((r = c->sig_grp.ensure(ns))) return r;
+    w.sig_grp = c->sig_grp.p;
   }
   w.msm_bucket = nullptr; w.msm_mask = nullptr; w.msm_win = nullptr;
   if (d.msm) {
@@ -568,10 +585,24 @@ static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int fro
         HIPCHK(hipStreamWaitEvent(st, dep[ST_HASH], 0));
     }
     if (timed) HIPCHK(hipEventRecord(c->ev[s], st));
+    // deferred subgroup checks: their verdicts enter the codes before the fold
+    if (s == ST_F_TREE && d.defer_grp) {
+      if (fork) HIPCHK(hipStreamWaitEvent(st, c->ev_grp, 0));
+      launch_sig_fixup(st, d, w);
+    }
     launch_stage(st, s, d, w);
     HIPCHK(hipGetLastError());
     if (timed) HIPCHK(hipEventRecord(c->ev_end[s], st));
     else if (fork && (s == ST_PK_SCALE || s == ST_HASH || s == ST_MILLER)) HIPCHK(hipEventRecord(c->ev_dep[s], st));
+    if (d.defer_grp && s == ST_SIG && fork) HIPCHK(hipEventRecord(c->ev_sigdec, st));
+    if (d.defer_grp && s == ST_PK_SCALE) {
+      // the pubkey stream is idle once the Miller loops have their keys: the
+      // checks run there, beside them (the Miller loops wait on the event above)
+      if (fork) HIPCHK(hipStreamWaitEvent(st, c->ev_sigdec, 0));
+      launch_sig_check(st, d, w);
+      HIPCHK(hipGetLastError());
+      if (fork) HIPCHK(hipEventRecord(c->ev_grp, st));
+    }
     return 0;
   };
   if (early_hash) {  // enqueued first, so the host's launch latency does not delay it either

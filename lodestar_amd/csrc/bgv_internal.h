@@ -25,6 +25,8 @@ struct dev_batch {
   uint32_t msm;             // 1: per-job bucket MSM for sum r_i sigma_i (k_msm_*), 0: per-set [r_i] sigma_i + tree
   uint32_t split;           // 1: latency mode: hash maps on two lanes per set, subgroup check beside [r_i] sigma_i
   uint32_t prefold_log2;    // >0: two-level job fold, groups of 2^prefold_log2 sets (k_job_prefold); 0: one level
+  uint32_t defer_grp;       // bulk mode: ST_SIG only decodes; the G2 subgroup check runs beside the Miller loops
+                            // (launch_sig_check) and its verdicts reach the job codes before the fold (launch_sig_fixup)
   const uint32_t* job_off;
   const uint32_t* pk_off;
   const uint32_t* pk_idx;
@@ -43,7 +45,7 @@ struct dev_work {
   int32_t* sig_code;  // parse / subgroup outcome
   g2a* h_aff;         // H(m)
   g2j* q_part;        // [2 n_sets] split mode: the two mapped points of every message
-  uint32_t* sig_grp;  // split mode: signature passed the subgroup check
+  uint32_t* sig_grp;  // split / defer_grp mode: signature passed the subgroup check
   g2j* msm_bucket;    // [n_jobs * 16 windows * 15 buckets] (msm mode)
   uint32_t* msm_mask; // [n_jobs * 16] occupied buckets of each (job, window)
   g2j* msm_win;       // [n_jobs * 16] window sums
@@ -95,6 +97,8 @@ void launch_pk_validate(hipStream_t st, const uint8_t* in, uint32_t n, int32_t* 
 void launch_prep(hipStream_t st, const dev_batch& b, const dev_work& w);  // before ST_PK / ST_MILLER
 void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work& w);
 void launch_miller(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_miller.hip
+void launch_sig_check(hipStream_t st, const dev_batch& b, const dev_work& w);   // subgroup checks only (sig_grp)
+void launch_sig_fixup(hipStream_t st, const dev_batch& b, const dev_work& w);   // k_sig_fix + k_job_recode
 void launch_sig_split_coop(hipStream_t st, const dev_batch& b, const dev_work& w);   // bgv_latency.hip
 void launch_hash_clear_coop(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_latency.hip
 void launch_fp12_tail(hipStream_t st, int stage, const dev_batch& b, const dev_work& w);  // bgv_tail.hip

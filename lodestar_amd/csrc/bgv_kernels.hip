@@ -284,6 +284,40 @@ __global__ void BGV_BULK k_sig_fix(dev_batch b, dev_work w) {
   }
 }
 
+// Deferred subgroup check (bulk mode, dev_batch.defer_grp).  The signature
+// stage only decodes, so the MSM starts ~60% sooner and phase 1 of the step
+// (hash, pubkeys, decode) carries ~1,200 fewer Fp products per set; the
+// checks run beside the set-pair Miller loops on the SIMDs it leaves free.
+// Their verdicts reach the codes before anything reads them: k_sig_fix marks
+// the failing signatures, k_job_recode re-derives every job's first failing
+// code (signatures first, then pubkeys, maybeBatch.ts:20-24) and gives a job
+// that only now fails the identity S_job and (-G1, S_job) value, exactly what
+// a job rejected at decode time has (k_msm_job / k_miller_coop), so the fold
+// leaves it out of the batch product.
+__global__ void BGV_BULK k_job_recode(dev_batch b, dev_work w) {
+  const uint32_t j = gtid();
+  if (j >= b.n_jobs) return;
+  // every job: a subgroup failure of an earlier set takes precedence over a
+  // decode failure of a later one (first failing code in set order)
+  const int32_t was = w.job_code[j];
+  const uint32_t beg = b.job_off[j], end = b.job_off[j + 1];
+  int32_t code = C_OK;
+  for (uint32_t i = beg; i < end && code == C_OK; i++) code = w.sig_code[i];
+  for (uint32_t i = beg; i < end && code == C_OK; i++) code = w.pk_code[i];
+  if (end == beg) code = C_EMPTY_JOB;
+  if (code == was) return;
+  w.job_code[j] = code;
+  if (was != C_OK) return;  // rejected at decode time: S_job and its pair are already the identity
+  g2a z;
+  z.x = fp2_zero();
+  z.y = fp2_zero();
+  w.s_aff[j] = z;
+  w.s_inf[j] = 1u;
+  fp12_t one;
+  fp12_one(one);
+  w.f_set[b.n_sets + j] = one;
+}
+
 // The cooperative G2 kernels of the latency mode (k_sig_split_coop,
 // k_hash_clear_coop) live in bgv_latency.hip: they run at 1 wave/SIMD, and
 // sharing this unit's non-inlined curve helpers with them raised k_sig to
@@ -943,6 +977,16 @@ static void launch_miller_coop(hipStream_t st, uint32_t lanes, const dev_batch& 
   }
 }
 
+void launch_sig_check(hipStream_t st, const dev_batch& b, const dev_work& w) {
+  const uint32_t nb = (b.n_sets + 63u) / 64u;  // k_sig_split's first nb blocks: the checks only
+  if (nb) hipLaunchKernelGGL(k_sig_split, dim3(nb), dim3(64), 0, st, b, w);
+}
+
+void launch_sig_fixup(hipStream_t st, const dev_batch& b, const dev_work& w) {
+  BGV_LAUNCH(k_sig_fix, b.n_sets, b, w);
+  BGV_LAUNCH(k_job_recode, b.n_jobs, b, w);
+}
+
 void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work& w) {
   const uint32_t span = 1u << b.span_log2;
   switch (stage) {
@@ -956,6 +1000,8 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
             hipLaunchKernelGGL(k_sig_split, dim3(2u * ((b.n_sets + 63u) / 64u)), dim3(64), 0, st, b, w);
         }
         BGV_LAUNCH(k_sig_fix, b.n_sets, b, w);
+      } else if (b.defer_grp) {
+        BGV_LAUNCH(k_sig_dec, b.n_sets, b, w);  // subgroup check later: launch_sig_check
       } else {
         BGV_LAUNCH(k_sig, b.n_sets, b, w);
       }

@@ -194,3 +194,19 @@ def test_c5_faulted_segment_host_resident(big):
     clean = np.nonzero(expect == 1)[0]
     sample = sorted(rng.choice(faulted, size=8, replace=False).tolist() + rng.choice(clean, size=8, replace=False).tolist())
     _cref_block_check(big, fa, sample, expect)
+
+
+def test_c5_half_segment_deferred_subgroup_checks(big):
+    """C4/2 (512 blocks, 50,176 sets: one pair per Miller item, so the bulk
+    path defers the G2 subgroup checks beside the Miller loops) with 2 %
+    faults of the four kinds: job verdicts and set codes as constructed,
+    including a subgroup failure ahead of a later decode failure in one job
+    (first failing code in set order)"""
+    a = bench.build_segment(list(range(512)))
+    fa, expect = bench.inject_faults(big, a, 0.02, SEED + 5000)
+    jr, sc = big.verify(fa)
+    assert jr.tolist() == expect.tolist()
+    assert set(np.unique(sc).tolist()) == {0, 1, 3}
+    jo = a["job_offsets"]
+    mixed = [j for j in range(512) if 3 in sc[jo[j]:jo[j + 1]].tolist() and 1 in sc[jo[j]:jo[j + 1]].tolist()]
+    assert any(expect[j] == -3 for j in mixed) and any(expect[j] == -1 for j in mixed)
