@@ -353,20 +353,26 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BGV_BENCH_REHEARSE=1: every rank on GPU 0 with gloo collectives, to
+    # rehearse the N > 1 path on a one-GPU box (RCCL refuses two ranks on one
+    # device); the driver's multi-GPU runs never set it
+    rehearse = os.environ.get("BGV_BENCH_REHEARSE") == "1"
+    gpu = 0 if rehearse else local
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        dist.init_process_group("gloo" if rehearse else "nccl")
+    dev = torch.device("cuda", gpu)
+    coll_dev = None if rehearse else dev  # where the collectives' tensors live
 
     if args.shard:  # per-stage timing events also for shards below 65,536 sets
         os.environ.setdefault("BGV_TIMING", "1")
     from lodestar_amd import native
     from lodestar_amd.dist import gather_job_results, select_jobs, shard_jobs, verify_sharded
 
-    d = native.Device(local)
+    d = native.Device(gpu)
     t0 = time.time()
     d.gen_keys(0, N_VALIDATORS, SEED)
     log(f"[bench] {N_VALIDATORS} keys generated in {time.time() - t0:.1f}s")
@@ -390,9 +396,9 @@ def main():
         if world == 1:
             jr, _ = d.verify(darr, on_device=True, want_set_codes=False)
             return bool((jr == 1).all())
-        valid, local_jr = verify_sharded(d, darr, dist, device=dev, on_device=True)
+        valid, local_jr = verify_sharded(d, darr, dist, device=coll_dev, on_device=True)
         if args.shard:  # every rank ends with the whole segment's per-block verdicts
-            full = gather_job_results(local_jr, shards, seg["n_jobs"], dist, device=dev)
+            full = gather_job_results(local_jr, shards, seg["n_jobs"], dist, device=coll_dev)
             return valid and bool((full == 1).all())
         return valid and bool((local_jr == 1).all())
 
@@ -415,10 +421,10 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=coll_dev if coll_dev is not None else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        okt = torch.tensor([1 if all_ok else 0], device=dev)
+        okt = torch.tensor([1 if all_ok else 0], device=coll_dev if coll_dev is not None else "cpu")
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         all_ok = bool(okt.item())
     total_sets = seg["n_sets"] * (1 if args.shard else world)
