@@ -72,7 +72,6 @@ struct bgv_ctx {
   int timing = -1;        // BGV_TIMING=0|1: per-stage timing events; -1 = only for batches >= 65,536 sets
   int defer = -1;         // BGV_DEFER bits (A/B): 1 = sig_scale after hash, 2 = sig after hash, 4 = pk stream low priority
   int defer_grp = -1;     // BGV_DEFER_GRP=0|1: bulk-mode subgroup checks beside the Miller loops; -1 = on
-  int hash2 = -1;         // BGV_HASH2=0|1: bulk-mode hash as map + clear launches (A/B); -1 = off
   bool timed = true;      // the last run_stages recorded per-stage events
   int run_from = 0, run_to = 0;  // stage range of the last run_stages (bgv_last_stats)
   hipStream_t st = nullptr, st_hash = nullptr, st_pk = nullptr;
@@ -184,7 +183,6 @@ int bgv_open(int device, bgv_ctx** out) {
   if (const char* o = getenv("BGV_TIMING")) c->timing = atoi(o) != 0 ? 1 : 0;
   if (const char* o = getenv("BGV_DEFER")) c->defer = atoi(o);
   if (const char* o = getenv("BGV_DEFER_GRP")) c->defer_grp = atoi(o) != 0 ? 1 : 0;
-  if (const char* o = getenv("BGV_HASH2")) c->hash2 = atoi(o) != 0 ? 1 : 0;
   // hash -> set-pair Miller is the critical path: its stream (and the pubkey
   // stream feeding it) get the highest priority, signature decode/scaling the
   // lowest (it only feeds the signature tree and the 1 pair per job)
@@ -480,7 +478,6 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   // (bgv_kernels.hip k_job_recode); the latency mode has its own split
   // (one pair per Miller item: C4/2 28.3 -> 26.4 ms; with two pairs per item
   // the checks slow the longer Miller phase more than they save: C4 40.4 -> 41.9)
-  d.hash2 = (!d.split && c->hash2 > 0) ? 1u : 0u;
   d.defer_grp = c->defer_grp >= 0 ? (uint32_t)(!d.split && c->defer_grp)
                                   : ((!d.split && d.pairs_per_item == 1) ? 1u : 0u);
   // two-level per-job fold (bgv_tail.hip) when few jobs of >= 64 sets leave
@@ -539,15 +536,9 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
   if (d.split) {
     if ((r = c->q_part.ensure(2 * ns)) || (r = c->sig_grp.ensure(ns))) return r;
     w.q_part = c->q_part.p; w.sig_grp = c->sig_grp.p;
-  } else {
-    if (d.defer_grp) {
-      if ((r = c->sig_grp.ensure(ns))) return r;
-      w.sig_grp = c->sig_grp.p;
-    }
-    if (d.hash2) {
-      if ((r = c->q_part.ensure(2 * ns))) return r;
-      w.q_part = c->q_part.p;
-    }
+  } else if (d.defer_grp) {
+    if ((r = c->sig_grp.ensure(ns))) return r;
+    w.sig_grp = c->sig_grp.p;
   }
   w.msm_bucket = nullptr; w.msm_mask = nullptr; w.msm_win = nullptr;
   if (d.msm) {

@@ -25,7 +25,6 @@ struct dev_batch {
   uint32_t msm;             // 1: per-job bucket MSM for sum r_i sigma_i (k_msm_*), 0: per-set [r_i] sigma_i + tree
   uint32_t split;           // 1: latency mode: hash maps on two lanes per set, subgroup check beside [r_i] sigma_i
   uint32_t prefold_log2;    // >0: two-level job fold, groups of 2^prefold_log2 sets (k_job_prefold); 0: one level
-  uint32_t hash2;           // bulk mode: hash_to_G2 as two launches (maps on two lanes per message, then one lane per set)
   uint32_t defer_grp;       // bulk mode: ST_SIG only decodes; the G2 subgroup check runs beside the Miller loops
                             // (launch_sig_check) and its verdicts reach the job codes before the fold (launch_sig_fixup)
   const uint32_t* job_off;

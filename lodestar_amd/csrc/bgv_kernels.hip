@@ -1014,9 +1014,6 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
         } else {
           BGV_LAUNCH(k_hash_clear, b.n_sets, b, w);
         }
-      } else if (b.hash2) {
-        BGV_LAUNCH(k_hash_map, 2u * b.n_sets, b, w);
-        BGV_LAUNCH(k_hash_clear, b.n_sets, b, w);
       } else {
         BGV_LAUNCH(k_hash, b.n_sets, b, w);
       }
