@@ -31,7 +31,70 @@ struct cscratch {
 #ifndef BGV_COOP_LDS_AS
 #define BGV_COOP_LDS_AS 1
 #endif
-#if BGV_COOP_LDS_AS
+#ifndef BGV_COOP_TREE
+#define BGV_COOP_TREE 1  // c_mul2: the output sums across lanes instead of a third round
+#endif
+#if BGV_COOP_LDS_AS && BGV_COOP_TREE
+// out = a * b in TWO rounds: lane l < 36 of round 2 takes the product pair
+// (i, j) = (l % 6, (l / 6 - l % 6) mod 6), so the six terms of output
+// coefficient k = l / 6 sit in lanes 6k .. 6k + 5 of wave 0; they are summed
+// across lanes (ds_bpermute, no barrier) in the same order as round 3 of the
+// three-round form, ((t0 + t1) + (t2 + t3)) + (t4 + t5), and lane 6k writes c_k
+__device__ __forceinline__ fp2_t c_pull(const fp2_t& v, uint32_t src) {
+  fp2_t r;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+    r.c0.l[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v.c0.l[k]);
+    r.c1.l[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v.c1.l[k]);
+  }
+  return r;
+}
+__device__ void c_mul(wfp12* out_, const wfp12* a_, const wfp12* b_, cscratch* s_) {
+  BGV_LDS wfp12* out = (BGV_LDS wfp12*)out_;
+  const BGV_LDS wfp12* a = (const BGV_LDS wfp12*)a_;
+  const BGV_LDS wfp12* b = (const BGV_LDS wfp12*)b_;
+  BGV_LDS cscratch* s = (BGV_LDS cscratch*)s_;
+  const uint32_t l = threadIdx.x;
+  if (l < 108) {
+    const uint32_t p = l / 3, q = l - 3 * p, i = p / 6, j = p - 6 * i;
+    fp_t u, v;
+    if (q == 0) {
+      u = lds_get(&a->c[i].c0);
+      v = lds_get(&b->c[j].c0);
+    } else if (q == 1) {
+      u = lds_get(&a->c[i].c1);
+      v = lds_get(&b->c[j].c1);
+    } else {
+      fp_add_lazy2(u, lds_get(&a->c[i].c0), lds_get(&a->c[i].c1), v, lds_get(&b->c[j].c0), lds_get(&b->c[j].c1));
+    }
+    fp_t r;
+    fp_mul(r, u, v);
+    lds_put(&s->p[l], r);
+  }
+  __syncthreads();
+  if (l < 64) {  // wave 0; lanes >= 36 carry dummies through the exchange
+    const uint32_t k = l / 6 < 6 ? l / 6 : 0u, i = l % 6, j = (k + 6 - i) % 6, pr = i * 6 + j;
+    const fp_t p0 = lds_get(&s->p[3 * pr]), p1 = lds_get(&s->p[3 * pr + 1]), p2 = lds_get(&s->p[3 * pr + 2]);
+    fp2_t t;
+    fp_t w;
+    fp_add_sub(w, p0, p1, t.c0, p0, p1);
+    fp_sub(t.c1, p2, w);
+    if (i + j >= 6) fp2_mul_xi(t, t);
+    const uint32_t src1 = l + 1 < 64 ? l + 1 : l, src2 = l + 2 < 64 ? l + 2 : l, src4 = l + 4 < 64 ? l + 4 : l;
+    fp2_t x = c_pull(t, src1);  // i even: t_i + t_(i+1)
+    fp2_add(t, t, x);
+    x = c_pull(t, src2);        // i = 0: (t0 + t1) + (t2 + t3)
+    fp2_t y = c_pull(t, src4);  // i = 0: t4 + t5
+    fp2_add(t, t, x);
+    fp2_add(t, t, y);
+    if (l < 36 && i == 0) {
+      lds_put(&out->c[k].c0, t.c0);
+      lds_put(&out->c[k].c1, t.c1);
+    }
+  }
+  __syncthreads();
+}
+#elif BGV_COOP_LDS_AS
 // c_mul is a non-inlined function whose operands all live in LDS: the
 // casts below make its accesses ds_read / ds_write (lds.h)
 __device__ void c_mul(wfp12* out_, const wfp12* a_, const wfp12* b_, cscratch* s_) {
