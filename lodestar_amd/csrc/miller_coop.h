@@ -142,15 +142,18 @@ __device__ __forceinline__ void coop_line_round(coop_grp_t<SUB, HALF>& g, uint32
   if constexpr (HALF == 2) {
   // half 0: f_k a0 and the w^2 term; half 1: the w^3 term (same sum order)
   if (active) {
+    // both halves run two product calls (half 1's second is a dummy into its
+    // own slot), so the wave pays two product latencies, not 2 + 1 in turn
+    const fp2_t* pa1 = h == 0 ? &g.f[k] : &g.f[(k + 3) % 6];
+    const fp2_t* pb1 = h == 0 ? &g.line[0] : &g.line[2];
+    COOP_PROD(pa1, pb1, h == 0 ? &g.r[k] : &g.ah[k][1]);
+    COOP_PROD(h == 0 ? &g.f[(k + 4) % 6] : pa1, h == 0 ? &g.line[1] : pb1, h == 0 ? &g.ah[k][0] : &g.a[k]);
     if (h == 0) {
-      COOP_PROD(&g.f[k], &g.line[0], &g.r[k]);
       acc = g.r[k];
-      COOP_PROD(&g.f[(k + 4) % 6], &g.line[1], &g.ah[k][0]);
       fp2_t t = g.ah[k][0];
       if (k < 2) fp2_mul_xi(t, t);
       fp2_add(acc, acc, t);
     } else {
-      COOP_PROD(&g.f[(k + 3) % 6], &g.line[2], &g.ah[k][1]);
       acc = g.ah[k][1];
       if (k < 3) fp2_mul_xi(acc, acc);
     }
