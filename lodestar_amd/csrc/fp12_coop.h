@@ -252,18 +252,14 @@ __device__ void c_frob(wfp12* out, const wfp12* a, int k, cscratch* s) {
     fp_t r;
     if (m == 0) {
       r = comp ? t.c1 : t.c0;
-    } else {  // (t0 + t1 i)(g0 + g1 i): component comp by two Fp products
+    } else {  // (t0 + t1 i)(g0 + g1 i): component comp by two Fp products, the same
+              // instruction stream on both components (operands selected, no branch)
       const fp2_t& g = FROB_G[k - 1][m - 1];
-      fp_t x, y;
-      if (comp == 0) {
-        fp_mul(x, t.c0, g.c0);
-        fp_mul(y, t.c1, g.c1);
-        fp_sub(r, x, y);
-      } else {
-        fp_mul(x, t.c0, g.c1);
-        fp_mul(y, t.c1, g.c0);
-        fp_add(r, x, y);
-      }
+      fp_t x, y, sum, diff;
+      fp_mul(x, t.c0, comp ? g.c1 : g.c0);
+      fp_mul(y, t.c1, comp ? g.c0 : g.c1);
+      fp_add_sub(sum, x, y, diff, x, y);
+      r = comp ? sum : diff;
     }
     s->p[l] = r;
   }
@@ -289,15 +285,129 @@ __device__ void c_pow_x(wfp12* out, const wfp12* a, wfp12* acc, cscratch* s) {
 // LDS, tower form) = f^(3 (p^12 - 1) / r), the cube of the textbook value
 // (the hard-part chain computes m^(3 (p^4 - p^2 + 1) / r); 3 is prime to r,
 // so the value is 1 exactly when the textbook one is).
+// Karatsuba Fp6 product terms of x * y (tower Fp6 = Fp2[v]/(v^3 - xi)):
+// term k of {x0 y0, x1 y1, x2 y2, (x1+x2)(y1+y2), (x0+x1)(y0+y1), (x0+x2)(y0+y2)}
+__device__ __forceinline__ void c6_term(fp2_t& r, const fp6_t& x, const fp6_t& y, uint32_t k) {
+  fp2_t a, b;
+  if (k < 3) {
+    a = k == 0 ? x.c0 : (k == 1 ? x.c1 : x.c2);
+    b = k == 0 ? y.c0 : (k == 1 ? y.c1 : y.c2);
+  } else {
+    const fp2_t& xa = k == 5 ? x.c0 : (k == 3 ? x.c1 : x.c0);
+    const fp2_t& xb = k == 3 ? x.c2 : (k == 4 ? x.c1 : x.c2);
+    const fp2_t& ya = k == 5 ? y.c0 : (k == 3 ? y.c1 : y.c0);
+    const fp2_t& yb = k == 3 ? y.c2 : (k == 4 ? y.c1 : y.c2);
+    fp2_add(a, xa, xb);
+    fp2_add(b, ya, yb);
+  }
+  fp2_mul(r, a, b);
+}
+// the Karatsuba recombination of fp6_mul from its six terms
+__device__ __forceinline__ void c6_combine(fp6_t& r, const fp2_t* t) {
+  fp2_t u, x;
+  fp2_sub(u, t[3], t[1]);
+  fp2_sub(u, u, t[2]);
+  fp2_mul_xi(u, u);
+  fp2_add(r.c0, u, t[0]);
+  fp2_sub(u, t[4], t[0]);
+  fp2_sub(u, u, t[1]);
+  fp2_mul_xi(x, t[2]);
+  fp2_add(r.c1, u, x);
+  fp2_sub(u, t[5], t[0]);
+  fp2_sub(u, u, t[2]);
+  fp2_add(r.c2, u, t[1]);
+}
+
+// Fp12 inversion over the workgroup (fp12_inv's formulas and values): the
+// Fp2 products of each level on separate lanes, the recombinations on few,
+// the one Fp inversion (divsteps) on lane 0.  ~8 product levels instead of
+// ~100 sequential products on one lane (263 us, tools/ubench_coop.hip).
+//   1 / (a0 + a1 w) = (a0 - a1 w) / (a0^2 - v a1^2)
+struct cinv_scratch {
+  fp6_t a0, a1, t, c, ti, r0, r1;
+  fp2_t n, ni;
+  fp_t nn;
+};
+__device__ void c_inv12(fp12_t* out, const fp12_t& f, cinv_scratch* v, cscratch* s) {
+  const uint32_t l = threadIdx.x;
+  fp2_t* q = s->q;  // 36 Fp2 slots
+  if (l == 0) { v->a0 = f.c0; v->a1 = f.c1; }
+  __syncthreads();
+  // a0^2 and a1^2: 12 Karatsuba terms
+  if (l < 12) c6_term(q[l], l < 6 ? v->a0 : v->a1, l < 6 ? v->a0 : v->a1, l % 6);
+  __syncthreads();
+  if (l == 0) {
+    fp6_t t0, t1;
+    c6_combine(t0, q);
+    c6_combine(t1, q + 6);
+    fp6_mul_v(t1, t1);
+    fp6_sub(v->t, t0, t1);
+  }
+  __syncthreads();
+  // fp6_inv: c0 = t0^2 - xi t1 t2, c1 = xi t2^2 - t0 t1, c2 = t1^2 - t0 t2
+  if (l < 6) {
+    const fp2_t* x[6] = {&v->t.c0, &v->t.c1, &v->t.c2, &v->t.c0, &v->t.c1, &v->t.c0};
+    const fp2_t* y[6] = {&v->t.c0, &v->t.c2, &v->t.c2, &v->t.c1, &v->t.c1, &v->t.c2};
+    fp2_mul(q[l], *x[l], *y[l]);
+  }
+  __syncthreads();
+  if (l < 3) {
+    fp2_t r, u;
+    if (l == 0) { fp2_mul_xi(u, q[1]); fp2_sub(r, q[0], u); v->c.c0 = r; }
+    else if (l == 1) { fp2_mul_xi(u, q[2]); fp2_sub(r, u, q[3]); v->c.c1 = r; }
+    else { fp2_sub(r, q[4], q[5]); v->c.c2 = r; }
+  }
+  __syncthreads();
+  // n = t0 c0 + xi (t2 c1 + t1 c2)
+  if (l < 3) {
+    const fp2_t* x[3] = {&v->t.c2, &v->t.c1, &v->t.c0};
+    const fp2_t* y[3] = {&v->c.c1, &v->c.c2, &v->c.c0};
+    fp2_mul(q[l], *x[l], *y[l]);
+  }
+  __syncthreads();
+  if (l == 0) {
+    fp2_t n, u;
+    fp2_add(u, q[0], q[1]);
+    fp2_mul_xi(u, u);
+    fp2_add(n, u, q[2]);
+    v->n = n;
+    // fp2_inv: n^-1 = conj(n) / (n0^2 + n1^2)
+    fp_t nn;
+    fp2_norm(nn, n);
+    fp_inv(nn, nn);
+    v->nn = nn;
+  }
+  __syncthreads();
+  if (l < 2) {
+    fp_t r;
+    fp_mul(r, l == 0 ? v->n.c0 : v->n.c1, v->nn);
+    if (l == 0) v->ni.c0 = r;
+    else fp_neg(v->ni.c1, r);
+  }
+  __syncthreads();
+  // t^-1 = c * n^-1
+  if (l < 3) fp2_mul(l == 0 ? v->ti.c0 : (l == 1 ? v->ti.c1 : v->ti.c2), l == 0 ? v->c.c0 : (l == 1 ? v->c.c1 : v->c.c2), v->ni);
+  __syncthreads();
+  // a0 t^-1 and a1 t^-1: 12 Karatsuba terms
+  if (l < 12) c6_term(q[l], l < 6 ? v->a0 : v->a1, v->ti, l % 6);
+  __syncthreads();
+  if (l < 2) {
+    fp6_t r;
+    c6_combine(r, q + 6 * l);
+    if (l == 0) out->c0 = r;
+    else fp6_neg(out->c1, r);
+  }
+  __syncthreads();
+}
+
 __device__ void c_final_exp(fp12_t* out, const fp12_t& f_in, cscratch* s) {
   const uint32_t l = threadIdx.x;
   wfp12 *t0 = &s->t[0], *t1 = &s->t[1], *y0 = &s->t[2], *y1 = &s->t[3], *y2 = &s->t[4], *acc = &s->t[5];
   __shared__ wfp12 fin, y3;
+  __shared__ cinv_scratch iv;
+  __shared__ fp12_t inv;
+  c_inv12(&inv, f_in, &iv, s);
   if (l == 0) {
-    // the one Fp12 inversion of the easy part stays on one lane (its Fp
-    // inversion is a divstep chain, fp.h)
-    fp12_t inv;
-    fp12_inv(inv, f_in);
     w_from_tower(*t0, inv);
     w_from_tower(fin, f_in);
   }

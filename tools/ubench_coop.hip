@@ -23,6 +23,25 @@ __global__ void __launch_bounds__(64) k_chain_add(fp_t* io, uint32_t iters) {
   io[threadIdx.x] = x;
 }
 
+// one lane: the Fp12 inversion at the start of the final exponentiation
+__global__ void __launch_bounds__(64) k_inv(const fp12_t* in, fp12_t* out, uint32_t iters) {
+  fp12_t x = in[0];
+  for (uint32_t k = 0; k < iters; k++) fp12_inv(x, x);
+  if (threadIdx.x == 0) out[0] = x;
+}
+
+// one workgroup: a whole final exponentiation (k_batch_final's body)
+__global__ void __launch_bounds__(128) k_fe(const fp12_t* in, fp12_t* out, uint32_t iters) {
+  __shared__ cscratch s;
+  fp12_t x = in[0];
+  for (uint32_t k = 0; k < iters; k++) {
+    __shared__ fp12_t r;
+    c_final_exp(&r, x, &s);
+    x = r;
+  }
+  if (threadIdx.x == 0) out[0] = x;
+}
+
 // mode 0: full c_mul; 1: round 1 only (108 products + barrier)
 __global__ void __launch_bounds__(128) k_cmul(const fp12_t* in, fp12_t* out, uint32_t iters, uint32_t mode) {
   __shared__ cscratch s;
@@ -81,7 +100,17 @@ int main() {
     (void)hipEventRecord(e0, 0);
     hipLaunchKernelGGL(k_cmul, dim3(1), dim3(128), 0, 0, fin, fout, 500u, mode);
     (void)hipEventRecord(e1, 0);
-    printf(" \"c_mul_mode%u_us\": %.3f%s\n", mode, time_ms(e0, e1) * 1e3 / 500, mode ? "}" : ",");
+    printf(" \"c_mul_mode%u_us\": %.3f,\n", mode, time_ms(e0, e1) * 1e3 / 500);
   }
+  hipLaunchKernelGGL(k_inv, dim3(1), dim3(64), 0, 0, fin, fout, 2u);
+  (void)hipEventRecord(e0, 0);
+  hipLaunchKernelGGL(k_inv, dim3(1), dim3(64), 0, 0, fin, fout, 20u);
+  (void)hipEventRecord(e1, 0);
+  printf(" \"fp12_inv_one_lane_us\": %.2f,\n", time_ms(e0, e1) * 1e3 / 20);
+  hipLaunchKernelGGL(k_fe, dim3(1), dim3(128), 0, 0, fin, fout, 1u);
+  (void)hipEventRecord(e0, 0);
+  hipLaunchKernelGGL(k_fe, dim3(1), dim3(128), 0, 0, fin, fout, 5u);
+  (void)hipEventRecord(e1, 0);
+  printf(" \"final_exp_128_lanes_us\": %.1f}\n", time_ms(e0, e1) * 1e3 / 5);
   return 0;
 }
