@@ -40,6 +40,13 @@ struct cscratch {
 // coefficient k = l / 6 sit in lanes 6k .. 6k + 5 of wave 0; they are summed
 // across lanes (ds_bpermute, no barrier) in the same order as round 3 of the
 // three-round form, ((t0 + t1) + (t2 + t3)) + (t4 + t5), and lane 6k writes c_k
+// value of v in lane src of this wave (ds_bpermute addresses lanes within the wave)
+__device__ __forceinline__ fp_t c_pull1(const fp_t& v, uint32_t src) {
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < NL; k++) r.l[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v.l[k]);
+  return r;
+}
 __device__ __forceinline__ fp2_t c_pull(const fp2_t& v, uint32_t src) {
   fp2_t r;
 #pragma unroll
@@ -72,25 +79,35 @@ __device__ void c_mul(wfp12* out_, const wfp12* a_, const wfp12* b_, cscratch* s
     lds_put(&s->p[l], r);
   }
   __syncthreads();
-  if (l < 64) {  // wave 0; lanes >= 36 carry dummies through the exchange
-    const uint32_t k = l / 6 < 6 ? l / 6 : 0u, i = l % 6, j = (k + 6 - i) % 6, pr = i * 6 + j;
+  {
+    // round 2, one Fp component per lane: wave comp (0 or 1) handles component
+    // comp of every output coefficient; lane m = 6k + i of the wave takes the
+    // product pair (i, j = k - i mod 6), whose Fp2 value is (P0 - P1) + (P2 - P0 - P1) u,
+    // times xi when i + j >= 6:  re: 2 P0 - P2,  im: P2 - 2 P1.  Its component is
+    // one addition and one subtraction, the six terms of c_k then sum across the
+    // lanes (ds_bpermute) as ((t0 + t1) + (t2 + t3)) + (t4 + t5)
+    const uint32_t comp = l >> 6, m = l & 63u;
+    const uint32_t k = m / 6 < 6 ? m / 6 : 0u, i = m % 6, j = (k + 6 - i) % 6, pr = i * 6 + j;
+    const bool xi = i + j >= 6;
     const fp_t p0 = lds_get(&s->p[3 * pr]), p1 = lds_get(&s->p[3 * pr + 1]), p2 = lds_get(&s->p[3 * pr + 2]);
-    fp2_t t;
-    fp_t w;
-    fp_add_sub(w, p0, p1, t.c0, p0, p1);
-    fp_sub(t.c1, p2, w);
-    if (i + j >= 6) fp2_mul_xi(t, t);
-    const uint32_t src1 = l + 1 < 64 ? l + 1 : l, src2 = l + 2 < 64 ? l + 2 : l, src4 = l + 4 < 64 ? l + 4 : l;
-    fp2_t x = c_pull(t, src1);  // i even: t_i + t_(i+1)
-    fp2_add(t, t, x);
-    x = c_pull(t, src2);        // i = 0: (t0 + t1) + (t2 + t3)
-    fp2_t y = c_pull(t, src4);  // i = 0: t4 + t5
-    fp2_add(t, t, x);
-    fp2_add(t, t, y);
-    if (l < 36 && i == 0) {
-      lds_put(&out->c[k].c0, t.c0);
-      lds_put(&out->c[k].c1, t.c1);
-    }
+    fp_t zero;
+    fp_set_zero(zero);
+    // w = a + b;  t = c - d
+    //   re, no xi: (P0 + 0) - P1     re, xi: (P0 + P0) - P2
+    //   im, no xi: P2 - (P0 + P1)    im, xi: P2 - (P1 + P1)
+    const fp_t& a = comp ? (xi ? p1 : p0) : p0;
+    const fp_t& b = comp ? p1 : (xi ? p0 : zero);
+    fp_t w, t;
+    fp_add(w, a, b);
+    fp_sub(t, comp ? p2 : w, comp ? w : (xi ? p2 : p1));
+    const uint32_t src1 = m + 1 < 64 ? l + 1 : l, src2 = m + 2 < 64 ? l + 2 : l, src4 = m + 4 < 64 ? l + 4 : l;
+    fp_t x = c_pull1(t, src1 & 63u);  // i even: t_i + t_(i+1)
+    fp_add(t, t, x);
+    x = c_pull1(t, src2 & 63u);        // i = 0: (t0 + t1) + (t2 + t3)
+    const fp_t y = c_pull1(t, src4 & 63u);  // i = 0: t4 + t5
+    fp_add(t, t, x);
+    fp_add(t, t, y);
+    if (m < 36 && i == 0) lds_put(comp ? &out->c[k].c1 : &out->c[k].c0, t);
   }
   __syncthreads();
 }
