@@ -35,25 +35,15 @@ struct cscratch {
 #define BGV_COOP_TREE 1  // c_mul2: the output sums across lanes instead of a third round
 #endif
 #if BGV_COOP_LDS_AS && BGV_COOP_TREE
-// out = a * b in TWO rounds: lane l < 36 of round 2 takes the product pair
-// (i, j) = (l % 6, (l / 6 - l % 6) mod 6), so the six terms of output
-// coefficient k = l / 6 sit in lanes 6k .. 6k + 5 of wave 0; they are summed
-// across lanes (ds_bpermute, no barrier) in the same order as round 3 of the
-// three-round form, ((t0 + t1) + (t2 + t3)) + (t4 + t5), and lane 6k writes c_k
+// out = a * b in TWO rounds: the 108 Fp products, then one Fp component per
+// lane (wave c = component c): lane m = 6k + i takes the product pair
+// (i, k - i mod 6), and the six terms of c_k sum across lanes 6k .. 6k + 5
+// (ds_bpermute, no barrier) as ((t0 + t1) + (t2 + t3)) + (t4 + t5)
 // value of v in lane src of this wave (ds_bpermute addresses lanes within the wave)
 __device__ __forceinline__ fp_t c_pull1(const fp_t& v, uint32_t src) {
   fp_t r;
 #pragma unroll
   for (int k = 0; k < NL; k++) r.l[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v.l[k]);
-  return r;
-}
-__device__ __forceinline__ fp2_t c_pull(const fp2_t& v, uint32_t src) {
-  fp2_t r;
-#pragma unroll
-  for (int k = 0; k < NL; k++) {
-    r.c0.l[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v.c0.l[k]);
-    r.c1.l[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v.c1.l[k]);
-  }
   return r;
 }
 __device__ void c_mul(wfp12* out_, const wfp12* a_, const wfp12* b_, cscratch* s_) {
