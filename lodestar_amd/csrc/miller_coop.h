@@ -94,7 +94,17 @@ __device__ __noinline__ void coop_prod(const fp2_t* a, const fp2_t* b, fp2_t* ou
 // LDS hand-off between the sub-lanes of one coefficient lane (same wave):
 // wait for this wave's LDS writes, and keep the compiler from moving memory
 // accesses across
+#ifndef BGV_COOP_SYNC
+#define BGV_COOP_SYNC 0
+#endif
+#if BGV_COOP_SYNC
+// a wave's LDS instructions execute in issue order, so a lane's read after
+// another lane's write in the same wave sees it: only the compiler must not
+// move LDS accesses across the exchange point
+__device__ __forceinline__ void coop_wave_sync() { __builtin_amdgcn_wave_barrier(); __asm__ volatile("" ::: "memory"); }
+#else
 __device__ __forceinline__ void coop_wave_sync() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+#endif
 
 // *out = *a * *b over the three sub-lanes q of lane k: q0 a0 b0, q1 a1 b1,
 // q2 (a0 + a1)(b0 + b1) (one leaf call on every lane), then q0 / q1 form

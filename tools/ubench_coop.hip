@@ -7,6 +7,7 @@
 #define BGV_FPMUL_CALL 0
 #include "../lodestar_amd/csrc/bgv_internal.h"
 #include "../lodestar_amd/csrc/fp12_coop.h"
+#include "../lodestar_amd/csrc/coop_g2.h"
 #include <stdio.h>
 
 using namespace bgv;
@@ -40,6 +41,30 @@ __global__ void __launch_bounds__(128) k_fe(const fp12_t* in, fp12_t* out, uint3
     x = r;
   }
   if (threadIdx.x == 0) out[0] = x;
+}
+
+// one wave, seven 9-lane groups: chains of cooperative G2 doublings / additions
+// (coop_g2.h), the latency of one round of the cofactor clearing
+__global__ void __launch_bounds__(64) k_cg(const fp12_t* in, fp12_t* out, uint32_t iters, uint32_t add) {
+  __shared__ cg_scratch S[CG_GROUPS];
+  const uint32_t l = threadIdx.x, g = l / CG_LANES < CG_GROUPS ? l / CG_LANES : CG_GROUPS - 1, r = l - g * CG_LANES;
+  const uint32_t s = r < CG_LANES ? r / 3 : 0, q = r < CG_LANES ? r % 3 : 0;
+  g2j p, a;
+  p.x = in[0].c0.c0;
+  p.y = in[0].c0.c1;
+  p.z = in[0].c0.c2;
+  a.x = in[1].c0.c0;
+  a.y = in[1].c0.c1;
+  a.z = in[1].c0.c2;
+  for (uint32_t k = 0; k < iters; k++) {
+    if (add) cg_add(&S[g], s, q, p, p, a);
+    else cg_dbl(&S[g], s, q, p, p);
+  }
+  if (l == 0) {
+    out[0].c0.c0 = p.x;
+    out[0].c0.c1 = p.y;
+    out[0].c0.c2 = p.z;
+  }
 }
 
 // c_mul's two rounds with clock64() stamps (lane 0 of each wave): t[w][0..5]
@@ -174,6 +199,13 @@ int main() {
       printf(" \"cmul_phase_cycles_wave%d\": {", w);
       for (int k = 0; k < 7; k++) printf("\"%s\": %.0f%s", nm[k], (double)h[w * 8 + k] / 500, k < 6 ? ", " : "},\n");
     }
+  }
+  for (uint32_t add = 0; add < 2; add++) {
+    hipLaunchKernelGGL(k_cg, dim3(1), dim3(64), 0, 0, fin, fout, 4u, add);
+    (void)hipEventRecord(e0, 0);
+    hipLaunchKernelGGL(k_cg, dim3(1), dim3(64), 0, 0, fin, fout, 400u, add);
+    (void)hipEventRecord(e1, 0);
+    printf(" \"cg_%s_us\": %.3f,\n", add ? "add_6_rounds" : "dbl_3_rounds", time_ms(e0, e1) * 1e3 / 400);
   }
   hipLaunchKernelGGL(k_inv, dim3(1), dim3(64), 0, 0, fin, fout, 2u);
   (void)hipEventRecord(e0, 0);
