@@ -91,11 +91,10 @@ __device__ __noinline__ void coop_prod(const fp2_t* a, const fp2_t* b, fp2_t* ou
   *out = r;
 }
 
-// LDS hand-off between the sub-lanes of one coefficient lane (same wave):
-// wait for this wave's LDS writes, and keep the compiler from moving memory
-// accesses across
+// LDS hand-off between lanes of one wave (every user is a one-wave
+// workgroup): BGV_COOP_SYNC 0 also waits for the wave's LDS writes
 #ifndef BGV_COOP_SYNC
-#define BGV_COOP_SYNC 0
+#define BGV_COOP_SYNC 1  // r02: cg doubling 7.63 -> 7.36 us, k_hash_clear_coop 1,473 -> 1,448 us, k_miller_coop 1,347 -> 1,325 us (C2 shape)
 #endif
 #if BGV_COOP_SYNC
 // a wave's LDS instructions execute in issue order, so a lane's read after
