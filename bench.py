@@ -103,6 +103,18 @@ def fpmul_counts():
     return json.load(open(p)) if os.path.exists(p) else None
 
 
+def lines_active(n_sets):
+    """Mirrors prepare() in bgv_api.hip: the one-lane Miller loop runs over
+    fixed-argument lines (BGV_LINES) when its items hold two pairs
+    (>= 65,536 sets unless BGV_PAIRS forces one); the lines are an untimed
+    step between the hash and Miller stages."""
+    e = os.environ.get("BGV_LINES")
+    if e is not None and e != "":
+        return e != "0" and n_sets >= 35000
+    p = os.environ.get("BGV_PAIRS")
+    return p == "2" or (p != "1" and n_sets >= 65536)
+
+
 # stage -> its main kernel (rocprofv3 name) for the PMC traffic lookup
 STAGE_KERNEL = {"sig_decode_subgroup": "k_sig", "hash_to_g2": "k_hash", "pk_gather": "k_pk_chunk",
                 "pk_aggregate_scale": "k_pk", "sig_scale": "k_msm_bucket", "sig_sum_tree": "k_msm_job",
@@ -456,13 +468,16 @@ def main():
         fpm_ms = d.bench_fpmul(256 * 256 * 8, 2048)
         fpm_rate = 256 * 256 * 8 * 2048 / (fpm_ms * 1e-3) / 1e9
         per_stage = {}
+        stage_counts = dict(counts["per_set"]) if counts else {}
+        if counts and lines_active(n_sets) and "per_set_lines" in counts:
+            stage_counts["miller_loop"] = counts["per_set_lines"]["miller_loop"]
         for k, ms in stage_ms.items():
             if ms <= 0:
                 continue
             e = {"ms": round(ms, 3), "share_of_step": round(ms / ms_per_step, 3)}
-            if counts and k in counts["per_set"]:
-                ach = counts["per_set"][k] * n_sets / (ms * 1e-3) / 1e9
-                e.update(fpmul_per_set=counts["per_set"][k], achieved_G_fpmul_per_s=round(ach, 3),
+            if k in stage_counts:
+                ach = stage_counts[k] * n_sets / (ms * 1e-3) / 1e9
+                e.update(fpmul_per_set=stage_counts[k], achieved_G_fpmul_per_s=round(ach, 3),
                          frac=round(ach / peak_fpmul, 4))
             per_stage[k] = e
         pk_refs = int(arrays["pk_offsets"][-1])
@@ -484,6 +499,9 @@ def main():
                 "mad_u64_lane_ops_per_s": mad_rate, "peak_fpmul28_G_per_s": round(mad_rate / 393 / 1e9, 3),
                 "fpmul_microbench_G_per_s": round(fpm_rate, 3),
                 "per_stage": per_stage, "pubkey_gather": gather,
+                "miller_lines": ({"active": True, "kernel_name": "k_lines", "fpmul_per_set": counts["per_set_lines"]["miller_lines"],
+                                  "note": "untimed step on the hash stream between hash_to_g2 and miller_loop"}
+                                 if counts and lines_active(n_sets) and "per_set_lines" in counts else {"active": False}),
                 "step_fpmul_G_per_s": round(counts["per_set_total"] * n_sets / (ms_per_step * 1e-3) / 1e9, 3) if counts else None}
 
     if rank == 0:

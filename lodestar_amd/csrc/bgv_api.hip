@@ -71,6 +71,7 @@ struct bgv_ctx {
   int pairs = 0;          // BGV_PAIRS=1|2 forces sets per Miller work item (A/B tests); 0 = by batch size
   int timing = -1;        // BGV_TIMING=0|1: per-stage timing events; -1 = only for batches >= 65,536 sets
   int defer = -1;         // BGV_DEFER bits (A/B): 1 = sig_scale after hash, 2 = sig after hash, 4 = pk stream low priority
+  int use_lines = -1;     // BGV_LINES=0|1: fixed-argument Miller lines in the one-lane loop; -1 = with two pairs per item
   int defer_grp = -1;     // BGV_DEFER_GRP=0|1: bulk-mode subgroup checks beside the Miller loops; -1 = on
   bool timed = true;      // the last run_stages recorded per-stage events
   int run_from = 0, run_to = 0;  // stage range of the last run_stages (bgv_last_stats)
@@ -121,6 +122,7 @@ struct bgv_ctx {
   dbuf<g1j> pk_part;
   dbuf<g2j> rsig, q_part;
   dbuf<uint32_t> sig_grp;
+  dbuf<fp2_t> lines;
   dbuf<fp12_t> f_set, f_job, f_batch, f_tmp, f_part;
   dbuf<uint32_t> set_job, s_inf, item_off, item_job;
   dbuf<g2a> s_aff;
@@ -183,6 +185,7 @@ int bgv_open(int device, bgv_ctx** out) {
   if (const char* o = getenv("BGV_TIMING")) c->timing = atoi(o) != 0 ? 1 : 0;
   if (const char* o = getenv("BGV_DEFER")) c->defer = atoi(o);
   if (const char* o = getenv("BGV_DEFER_GRP")) c->defer_grp = atoi(o) != 0 ? 1 : 0;
+  if (const char* o = getenv("BGV_LINES")) c->use_lines = atoi(o) != 0 ? 1 : 0;
   // hash -> set-pair Miller is the critical path: its stream (and the pubkey
   // stream feeding it) get the highest priority, signature decode/scaling the
   // lowest (it only feeds the signature tree and the 1 pair per job)
@@ -228,7 +231,7 @@ int bgv_close(bgv_ctx* c) {
   c->scalars.release(); c->raw_conv.release();
   c->sig_aff.release(); c->h_aff.release(); c->sig_inf.release(); c->flags.release();
   c->sig_code.release(); c->pk_code.release(); c->job_code.release(); c->job_result.release(); c->set_code.release();
-  c->rpk_aff.release(); c->chunk_off.release(); c->chunk_set.release(); c->pk_part.release(); c->rsig.release(); c->q_part.release(); c->sig_grp.release(); c->f_set.release(); c->f_job.release(); c->f_batch.release(); c->f_tmp.release(); c->f_part.release();
+  c->rpk_aff.release(); c->chunk_off.release(); c->chunk_set.release(); c->pk_part.release(); c->rsig.release(); c->q_part.release(); c->sig_grp.release(); c->lines.release(); c->f_set.release(); c->f_job.release(); c->f_batch.release(); c->f_tmp.release(); c->f_part.release();
   c->msm_bucket.release(); c->msm_win.release(); c->msm_mask.release();
   c->set_job.release(); c->s_inf.release(); c->item_off.release(); c->item_job.release(); c->s_aff.release();
   c->mb_fp.release(); c->mb_u64.release();
@@ -489,6 +492,10 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
     d.prefold_log2 = on ? (d.span_log2 + 1) / 2 : 0u;
   }
   d.miller_coop = c->miller_mode >= 0 ? (uint32_t)c->miller_mode : (n < MILLER_COOP_MAX ? 36u : 0u);
+  // fixed-argument lines (pairing.h miller_lines): the G2 half of the one-lane
+  // Miller loop moves to the hash stream, phase 1 (C4 40.4 -> 39.5 ms); with
+  // one pair per item it loses (C4/2 26.4 -> 28.5 ms)
+  d.lines = (uint32_t)(!d.split && !d.miller_coop && (c->use_lines >= 0 ? c->use_lines : d.pairs_per_item == 2));
   d.job_lanes = c->job_lanes ? (uint32_t)c->job_lanes : 36u;
   // sum r_i sigma_i per job by a bucket MSM (16 x 4-bit windows, ~1,800 G2
   // additions per 98-set job instead of 98 x 75 in per-set scalar mults)
@@ -540,6 +547,11 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
     if ((r = c->sig_grp.ensure(ns))) return r;
     w.sig_grp = c->sig_grp.p;
   }
+  w.lines = nullptr;
+  if (d.lines) {
+    if ((r = c->lines.ensure((size_t)3 * MILLER_STEPS * ns))) return r;
+    w.lines = c->lines.p;
+  }
   w.msm_bucket = nullptr; w.msm_mask = nullptr; w.msm_win = nullptr;
   if (d.msm) {
     if ((r = c->msm_bucket.ensure(nj * 16 * 15)) || (r = c->msm_mask.ensure(nj * 16)) || (r = c->msm_win.ensure(nj * 16))) return r;
@@ -576,6 +588,12 @@ static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int fro
   const bool early_hash = fork && d.split && from <= ST_HASH && to > ST_HASH;
   auto launch_one = [&](int s) -> int {
     hipStream_t st = c->st;
+    // fixed-argument lines: right behind the hash on its stream, before the
+    // Miller stage waits for the pubkeys (timed in neither stage)
+    if (s == ST_MILLER && d.lines) {
+      launch_lines(fork ? c->st_hash : c->st, d, w);  // bgv_miller.hip
+      HIPCHK(hipGetLastError());
+    }
     if (fork) {
       if (s == ST_HASH || s == ST_MILLER) st = c->st_hash;
       if (s == ST_PK || s == ST_PK_SCALE) st = c->st_pk;

@@ -25,6 +25,8 @@ struct dev_batch {
   uint32_t msm;             // 1: per-job bucket MSM for sum r_i sigma_i (k_msm_*), 0: per-set [r_i] sigma_i + tree
   uint32_t split;           // 1: latency mode: hash maps on two lanes per set, subgroup check beside [r_i] sigma_i
   uint32_t prefold_log2;    // >0: two-level job fold, groups of 2^prefold_log2 sets (k_job_prefold); 0: one level
+  uint32_t lines;           // one-lane Miller loop over fixed-argument lines: the hash stream stores every set's
+                            // 68 unevaluated lines (launch_lines), k_miller evaluates them at P (pairing.h)
   uint32_t defer_grp;       // bulk mode: ST_SIG only decodes; the G2 subgroup check runs beside the Miller loops
                             // (launch_sig_check) and its verdicts reach the job codes before the fold (launch_sig_fixup)
   const uint32_t* job_off;
@@ -61,6 +63,7 @@ struct dev_work {
   uint32_t* item_job; // job of every Miller work item
   g2a* s_aff;         // per job: sum [r_i] sigma_i, affine
   uint32_t* s_inf;
+  fp2_t* lines;       // [68 steps][3][n_sets] unevaluated Miller lines of H(m_i) (dev_batch.lines)
   fp12_t* f_set;      // per pair Miller value: n_sets set pairs, then n_jobs (-G1, S_job) pairs
   fp12_t* f_job;      // per-job Miller product (incl. the -G1 pair)
   fp12_t* f_batch;    // batch product scratch [n_jobs]; the product ends in f_batch[0]
@@ -97,6 +100,7 @@ void launch_pk_validate(hipStream_t st, const uint8_t* in, uint32_t n, int32_t* 
 void launch_prep(hipStream_t st, const dev_batch& b, const dev_work& w);  // before ST_PK / ST_MILLER
 void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work& w);
 void launch_miller(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_miller.hip
+void launch_lines(hipStream_t st, const dev_batch& b, const dev_work& w);   // bgv_miller.hip
 void launch_sig_check(hipStream_t st, const dev_batch& b, const dev_work& w);   // subgroup checks only (sig_grp)
 void launch_sig_fixup(hipStream_t st, const dev_batch& b, const dev_work& w);   // k_sig_fix + k_job_recode
 void launch_sig_split_coop(hipStream_t st, const dev_batch& b, const dev_work& w);   // bgv_latency.hip

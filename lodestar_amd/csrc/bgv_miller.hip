@@ -60,6 +60,7 @@ __global__ void __launch_bounds__(64, BGV_MILLER_WAVES) k_miller(dev_batch b, de
     // a parse error rejects the whole job, so its Miller values are never used;
     // signature codes are not known yet (this part overlaps ST_SIG_SCALE)
     if (!ok1 || !ok2) fp12_one(f);
+    else if (b.lines) miller_loop_lines(f, w.lines, b.n_sets, w.rpk_aff[i1], i1, w.rpk_aff[two ? i1 + 1 : i1], i1 + 1, two);
     else if (two) miller_loop2(f, w.rpk_aff[i1], w.h_aff[i1], w.rpk_aff[i1 + 1], w.h_aff[i1 + 1]);
     else miller_loop(f, w.rpk_aff[i1], false, w.h_aff[i1], false);
     w.f_set[i1] = f;
@@ -76,6 +77,18 @@ __global__ void __launch_bounds__(64, BGV_MILLER_WAVES) k_miller(dev_batch b, de
     else miller_loop(f, ng, false, w.s_aff[j], false);
     w.f_set[b.n_sets + j] = f;
   }
+}
+
+// the unevaluated lines of every set's H(m) (pairing.h miller_lines), on the
+// hash stream right after k_hash: one lane per set
+__global__ void __launch_bounds__(64, 2) k_lines(dev_batch b, dev_work w) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= b.n_sets) return;
+  miller_lines(w.lines, b.n_sets, i, w.h_aff[i]);
+}
+
+void launch_lines(hipStream_t st, const dev_batch& b, const dev_work& w) {
+  if (b.n_sets) hipLaunchKernelGGL(k_lines, dim3((b.n_sets + 63u) / 64u), dim3(64), 0, st, b, w);
 }
 
 void launch_miller(hipStream_t st, const dev_batch& b, const dev_work& w) {

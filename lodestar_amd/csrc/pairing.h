@@ -36,8 +36,11 @@ BGV_HD void fp2_mul_3b(fp2_t& r, const fp2_t& a) {
   fp2_mul3(r, t);
 }
 
-// T <- 2T, line tangent at T evaluated at P
-BGV_NIS void miller_dbl_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const fp_t& xp, const fp_t& yp) {
+// T <- 2T, line tangent at T evaluated at P.  With AT_P false the line is
+// left unevaluated (fixed-argument form, BGV_LINES): a1 = 3X^2 and b1 = 2YZ,
+// and miller_line_at_p applies the same P factors later.
+template <bool AT_P>
+BGV_HD void miller_dbl_core(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const fp_t& xp, const fp_t& yp) {
   fp2_t A, B, C, E, F, G, H, t;
   fp2_mul(A, T.x, T.y);
   fp_half(A.c0, A.c0);
@@ -54,9 +57,14 @@ BGV_NIS void miller_dbl_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const fp
   fp2_sub(a0, E, B);
   fp2_sqr(t, T.x);
   fp2_mul3(t, t);
-  fp2_mul_fp(a1, t, xp);
-  fp2_mul_fp(t, H, yp);
-  fp2_neg(b1, t);
+  if constexpr (AT_P) {
+    fp2_mul_fp(a1, t, xp);
+    fp2_mul_fp(t, H, yp);
+    fp2_neg(b1, t);
+  } else {
+    a1 = t;
+    b1 = H;
+  }
   // point
   fp2_sub(t, B, F);
   fp2_mul(T.x, A, t);            // X3 = XY/2 (Y^2 - 9b'Z^2)
@@ -69,10 +77,15 @@ BGV_NIS void miller_dbl_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const fp
   fp2_sub(T.y, G, t);
   fp2_mul(T.z, B, H);            // Z3 = 2 Y^3 Z
 }
+BGV_NIS void miller_dbl_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const fp_t& xp, const fp_t& yp) {
+  miller_dbl_core<true>(T, a0, a1, b1, xp, yp);
+}
 
-// T <- T + Q (Q affine), line through T and Q evaluated at P
-BGV_NIS void miller_add_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const g2a& Q, const fp_t& xp,
-                            const fp_t& yp) {
+// T <- T + Q (Q affine), line through T and Q evaluated at P (AT_P false:
+// a1 = theta, b1 = lambda, for miller_line_at_p)
+template <bool AT_P>
+BGV_HD void miller_add_core(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const g2a& Q,
+                                                const fp_t& xp, const fp_t& yp) {
   fp2_t th, la, C, D, E, F, G, H, t;
   fp2_mul(t, Q.y, T.z);
   fp2_sub(th, T.y, t);           // theta = Y - yQ Z
@@ -82,9 +95,14 @@ BGV_NIS void miller_add_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const g2
   fp2_mul(a0, th, Q.x);
   fp2_mul(t, la, Q.y);
   fp2_sub(a0, a0, t);
-  fp2_mul_fp(t, th, xp);
-  fp2_neg(a1, t);
-  fp2_mul_fp(b1, la, yp);
+  if constexpr (AT_P) {
+    fp2_mul_fp(t, th, xp);
+    fp2_neg(a1, t);
+    fp2_mul_fp(b1, la, yp);
+  } else {
+    a1 = th;
+    b1 = la;
+  }
   // point
   fp2_sqr(C, th);
   fp2_sqr(D, la);
@@ -100,6 +118,56 @@ BGV_NIS void miller_add_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const g2
   fp2_mul(C, T.y, E);
   fp2_sub(T.y, t, C);
   fp2_mul(T.z, T.z, E);
+}
+BGV_NIS void miller_add_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const g2a& Q, const fp_t& xp,
+                            const fp_t& yp) {
+  miller_add_core<true>(T, a0, a1, b1, Q, xp, yp);
+}
+
+// Fixed-argument lines (BGV_LINES): the 68 lines of Q's Miller loop (63
+// doublings, 5 additions), unevaluated, stored per step as (a0, a1, b1) at
+// lines[(3 step + c) stride + i]; miller_line_at_p finishes one at P with
+// the operations the steps above apply, so f is bit-identical.
+constexpr int MILLER_STEPS = 68;
+BGV_NI void miller_lines(fp2_t* lines, uint32_t stride, uint32_t i, const g2a& Q) {
+  g2p_t T;
+  T.x = Q.x;
+  T.y = Q.y;
+  T.z = fp2_one();
+  fp2_t a0, a1, b1;
+  fp_t zero;
+  fp_set_zero(zero);
+  uint32_t s = 0;
+  for (int b = 62; b >= 0; b--) {
+    miller_dbl_core<false>(T, a0, a1, b1, zero, zero);
+    lines[(size_t)(3 * s) * stride + i] = a0;
+    lines[(size_t)(3 * s + 1) * stride + i] = a1;
+    lines[(size_t)(3 * s + 2) * stride + i] = b1;
+    s++;
+    if ((BLS_X_ABS >> b) & 1ull) {
+      miller_add_core<false>(T, a0, a1, b1, Q, zero, zero);
+      lines[(size_t)(3 * s) * stride + i] = a0;
+      lines[(size_t)(3 * s + 1) * stride + i] = a1;
+      lines[(size_t)(3 * s + 2) * stride + i] = b1;
+      s++;
+    }
+  }
+}
+
+BGV_HD void miller_line_at_p(fp2_t& a0, fp2_t& a1, fp2_t& b1, const fp2_t* lines, uint32_t stride,
+                                                 uint32_t i, uint32_t s, bool add, const fp_t& xp, const fp_t& yp) {
+  fp2_t t;
+  a0 = lines[(size_t)(3 * s) * stride + i];
+  const fp2_t c1 = lines[(size_t)(3 * s + 1) * stride + i], c2 = lines[(size_t)(3 * s + 2) * stride + i];
+  if (!add) {
+    fp2_mul_fp(a1, c1, xp);
+    fp2_mul_fp(t, c2, yp);
+    fp2_neg(b1, t);
+  } else {
+    fp2_mul_fp(t, c1, xp);
+    fp2_neg(a1, t);
+    fp2_mul_fp(b1, c2, yp);
+  }
 }
 
 // f = f_{x, Q}(P) for the negative x (conjugated), P affine in G1, Q affine in G2.
@@ -160,6 +228,40 @@ BGV_NIL void miller_loop2(fp12_t& f, const g1a& P1, const g2a& Q1, const g1a& P2
       fp12_mul_line(f, f, a0, a1, b1);
       miller_add_step(T2, a0, a1, b1, Q2, P2.x, P2.y);
       fp12_mul_line(f, f, a0, a1, b1);
+    }
+  }
+  fp12_conj(f, f);  // x < 0
+}
+
+// miller_loop2 (two = true) / miller_loop over precomputed lines of sets i1, i2
+BGV_NIL void miller_loop_lines(fp12_t& f, const fp2_t* lines, uint32_t stride, const g1a& P1, uint32_t i1,
+                               const g1a& P2, uint32_t i2, bool two) {
+  fp2_t a0, a1, b1;
+  fp12_one(f);
+  uint32_t s = 0;
+  for (int b = 62; b >= 0; b--) {
+    if (b != 62) fp12_sqr(f, f);
+    miller_line_at_p(a0, a1, b1, lines, stride, i1, s, false, P1.x, P1.y);
+    if (b == 62) {  // f = 1 * line
+      f.c0.c0 = a0;
+      f.c0.c1 = a1;
+      f.c1.c1 = b1;
+    } else {
+      fp12_mul_line(f, f, a0, a1, b1);
+    }
+    if (two) {
+      miller_line_at_p(a0, a1, b1, lines, stride, i2, s, false, P2.x, P2.y);
+      fp12_mul_line(f, f, a0, a1, b1);
+    }
+    s++;
+    if ((BLS_X_ABS >> b) & 1ull) {
+      miller_line_at_p(a0, a1, b1, lines, stride, i1, s, true, P1.x, P1.y);
+      fp12_mul_line(f, f, a0, a1, b1);
+      if (two) {
+        miller_line_at_p(a0, a1, b1, lines, stride, i2, s, true, P2.x, P2.y);
+        fp12_mul_line(f, f, a0, a1, b1);
+      }
+      s++;
     }
   }
   fp12_conj(f, f);  // x < 0

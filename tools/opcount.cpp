@@ -6,10 +6,12 @@
 #define BGV_COUNT_OPS 1
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 #include "../lodestar_amd/csrc/pairing.h"
 namespace bgv { unsigned long long bgv_fpmul_count = 0; }
 using namespace bgv;
 
+static int lines_mismatch = 0;
 static uint64_t rng = 0x243f6a8885a308d3ull;
 static uint64_t rnd64() { rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17; return rng; }
 
@@ -28,7 +30,7 @@ int main(int argc, char** argv) {
     for (int i = 0; i < 64; i++) { jac_dbl(acc, acc); jac_add(acc, acc, g); jac_to_aff(pts[i], acc); } }
 
   const int reps = 64;
-  double sig_c = 0, hash_c = 0, pk_add_c = 0, pk_fix_c = 0, sig_scale_c = 0, miller_c = 0, miller2_c = 0, fmul_c = 0, g2add_c = 0, aff2_c = 0, fe_c = 0;
+  double sig_c = 0, hash_c = 0, pk_add_c = 0, pk_fix_c = 0, sig_scale_c = 0, miller_c = 0, miller2_c = 0, lines_c = 0, loopl2_c = 0, fmul_c = 0, g2add_c = 0, aff2_c = 0, fe_c = 0;
   for (int r = 0; r < reps; r++) {
     uint64_t sc = rnd64() | (1ull << 63);  // full 64-bit random scalar (top bit set: worst case)
     sc = rnd64(); if (!sc) sc = 1;
@@ -61,6 +63,15 @@ int main(int argc, char** argv) {
     bgv_fpmul_count = 0;
     fp12_t f2; miller_loop2(f2, rpa, ha, rpa, ha);  // C4 (n >= 65536): two sets per work item
     miller2_c += bgv_fpmul_count;
+    // fixed-argument lines (BGV_LINES, C4): lines of H(m) on the hash stream, then the loop over them
+    static fp2_t lines[3 * MILLER_STEPS];
+    bgv_fpmul_count = 0;
+    miller_lines(lines, 1, 0, ha);
+    lines_c += bgv_fpmul_count;
+    bgv_fpmul_count = 0;
+    fp12_t f3; miller_loop_lines(f3, lines, 1, rpa, 0, rpa, 0, true);
+    loopl2_c += bgv_fpmul_count;
+    if (memcmp(&f3, &f2, sizeof f2) != 0) lines_mismatch++;
     bgv_fpmul_count = 0;
     fp12_t g; fp12_mul(g, f, f);
     fmul_c += bgv_fpmul_count;
@@ -99,7 +110,7 @@ int main(int argc, char** argv) {
     g2a sa; jac_to_aff(sa, s);
     msm_c = (double)bgv_fpmul_count / per_block;
   }
-  sig_c /= reps; hash_c /= reps; pk_add_c /= reps; pk_fix_c /= reps; sig_scale_c /= reps; miller_c /= reps; miller2_c /= reps;
+  sig_c /= reps; hash_c /= reps; pk_add_c /= reps; pk_fix_c /= reps; sig_scale_c /= reps; miller_c /= reps; miller2_c /= reps; lines_c /= reps; loopl2_c /= reps;
   fmul_c /= reps; g2add_c /= reps; aff2_c /= reps;
   // C4 block mix: 95 sets of k=128, 1 of k=512, 2 singles -> mean pubkeys per set
   const double mean_k = (95.0 * k_att + k_sync + 2.0) / per_block;
@@ -125,6 +136,11 @@ int main(int argc, char** argv) {
   printf(" \"per_set\": {\"sig_decode_subgroup\": %.1f, \"hash_to_g2\": %.1f, \"pk_gather\": %.1f, \"pk_aggregate_scale\": %.1f, "
          "\"sig_scale\": %.1f, \"sig_sum_tree\": %.1f, \"miller_loop\": %.1f, \"miller_loop_jobs\": %.1f, \"miller_product_tree\": %.1f},\n",
          sig_c, hash_c, pk_gather, pk_fix_c, msm_bucket_c, s_tree, miller_set, miller_jobs, f_tree);
-  printf(" \"per_set_total\": %.1f\n}\n", sig_c + hash_c + pk_c + msm_c + miller_set + miller_jobs + f_tree);
+  // fixed-argument lines at C4: the lines are their own (untimed) step, the
+  // Miller stage loops over them; the two-pair value is bit-identical
+  printf(" \"per_set_lines\": {\"miller_lines\": %.1f, \"miller_loop\": %.1f, \"loop_values_match\": %s},\n",
+         lines_c, loopl2_c / 2.0, lines_mismatch ? "false" : "true");
+  printf(" \"per_set_total\": %.1f,\n", sig_c + hash_c + pk_c + msm_c + miller_set + miller_jobs + f_tree);
+  printf(" \"per_set_total_lines\": %.1f\n}\n", sig_c + hash_c + pk_c + msm_c + lines_c + loopl2_c / 2.0 + miller_jobs + f_tree);
   return 0;
 }
