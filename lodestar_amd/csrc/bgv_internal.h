@@ -27,6 +27,7 @@ struct dev_batch {
   uint32_t prefold_log2;    // >0: two-level job fold, groups of 2^prefold_log2 sets (k_job_prefold); 0: one level
   uint32_t lines;           // one-lane Miller loop over fixed-argument lines: the hash stream stores every set's
                             // 68 unevaluated lines (launch_lines), k_miller evaluates them at P (pairing.h)
+  uint32_t defer_from;      // defer_grp: sets below it are checked in ST_SIG as usual, the rest later (multiple of 64)
   uint32_t defer_grp;       // bulk mode: ST_SIG only decodes; the G2 subgroup check runs beside the Miller loops
                             // (launch_sig_check) and its verdicts reach the job codes before the fold (launch_sig_fixup)
   const uint32_t* job_off;

@@ -212,7 +212,9 @@ __global__ void __launch_bounds__(64, BGV_SIG_WAVES) k_sig(dev_batch b, dev_work
   if (len == 96u) code = g2_decompress(a, inf, s);
   else if (len == 192u) code = g2_deserialize(a, inf, s);
   else code = C_INVALID_SIZE;
-  if (code == C_OK && !inf) {
+  // partial deferral (dev_batch.defer_from): sets from defer_from on are
+  // checked later by launch_sig_check (wave-uniform: a multiple of 64)
+  if (code == C_OK && !inf && !(b.defer_grp && i >= b.defer_from)) {
     g2j j;
     jac_from_aff(j, a);
     if (!g2_in_subgroup(j)) code = C_POINT_NOT_IN_GROUP;
@@ -248,7 +250,8 @@ __global__ void __launch_bounds__(64, BGV_SIG_WAVES) k_sig_dec(dev_batch b, dev_
 __global__ void __launch_bounds__(64, BGV_SIG_WAVES) k_sig_split(dev_batch b, dev_work w) {
   const uint32_t nb = (b.n_sets + 63u) / 64u;
   const bool check = blockIdx.x < nb;
-  const uint32_t i = (check ? blockIdx.x : blockIdx.x - nb) * 64u + threadIdx.x;
+  // deferred checks (launch_sig_check) start at defer_from
+  const uint32_t i = (check ? blockIdx.x : blockIdx.x - nb) * 64u + threadIdx.x + (check && b.defer_grp ? b.defer_from : 0u);
   if (i >= b.n_sets) return;
   const bool live = w.sig_code[i] == C_OK && !w.sig_inf[i];  // decode outcome (k_sig_dec)
   if (check) {
@@ -274,7 +277,7 @@ __global__ void __launch_bounds__(64, BGV_SIG_WAVES) k_sig_split(dev_batch b, de
 
 __global__ void BGV_BULK k_sig_fix(dev_batch b, dev_work w) {
   const uint32_t i = gtid();
-  if (i >= b.n_sets) return;
+  if (i >= b.n_sets || (b.defer_grp && i < b.defer_from)) return;  // checked in ST_SIG
   if (w.sig_code[i] == C_OK && !w.sig_grp[i]) {
     w.sig_code[i] = C_POINT_NOT_IN_GROUP;
     g2a z;
@@ -978,8 +981,9 @@ static void launch_miller_coop(hipStream_t st, uint32_t lanes, const dev_batch& 
 }
 
 void launch_sig_check(hipStream_t st, const dev_batch& b, const dev_work& w) {
-  const uint32_t nb = (b.n_sets + 63u) / 64u;  // k_sig_split's first nb blocks: the checks only
-  if (nb) hipLaunchKernelGGL(k_sig_split, dim3(nb), dim3(64), 0, st, b, w);
+  // k_sig_split's check blocks only, for the sets from defer_from on
+  const uint32_t nd = (b.n_sets - b.defer_from + 63u) / 64u;
+  if (nd) hipLaunchKernelGGL(k_sig_split, dim3(nd), dim3(64), 0, st, b, w);
 }
 
 void launch_sig_fixup(hipStream_t st, const dev_batch& b, const dev_work& w) {
@@ -1000,7 +1004,7 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
             hipLaunchKernelGGL(k_sig_split, dim3(2u * ((b.n_sets + 63u) / 64u)), dim3(64), 0, st, b, w);
         }
         BGV_LAUNCH(k_sig_fix, b.n_sets, b, w);
-      } else if (b.defer_grp) {
+      } else if (b.defer_grp && b.defer_from == 0) {
         BGV_LAUNCH(k_sig_dec, b.n_sets, b, w);  // subgroup check later: launch_sig_check
       } else {
         BGV_LAUNCH(k_sig, b.n_sets, b, w);
