@@ -115,6 +115,24 @@ def lines_active(n_sets):
     return p == "2" or (p != "1" and n_sets >= 65536)
 
 
+def defer_share(n_sets):
+    """Mirrors prepare() in bgv_api.hip: the share of the sets whose G2
+    subgroup check leaves the signature stage for the SIMDs beside the Miller
+    loops (k_sig_split, untimed): half at two pairs per item, all between
+    35,000 and 65,535 sets, none below (latency mode)."""
+    if n_sets < 35000:
+        return 0.0
+    e = os.environ.get("BGV_DEFER_PCT")
+    if e:
+        return min(max(int(e), 0), 100) / 100.0
+    g = os.environ.get("BGV_DEFER_GRP")
+    p = os.environ.get("BGV_PAIRS")
+    two = p == "2" or (p != "1" and n_sets >= 65536)
+    if g:
+        return (0.5 if two else 1.0) if g != "0" else 0.0
+    return 0.5 if two else 1.0
+
+
 # stage -> its main kernel (rocprofv3 name) for the PMC traffic lookup
 STAGE_KERNEL = {"sig_decode_subgroup": "k_sig", "hash_to_g2": "k_hash", "pk_gather": "k_pk_chunk",
                 "pk_aggregate_scale": "k_pk", "sig_scale": "k_msm_bucket", "sig_sum_tree": "k_msm_job",
@@ -471,6 +489,11 @@ def main():
         stage_counts = dict(counts["per_set"]) if counts else {}
         if counts and lines_active(n_sets) and "per_set_lines" in counts:
             stage_counts["miller_loop"] = counts["per_set_lines"]["miller_loop"]
+        share = defer_share(n_sets)
+        check_c = None
+        if counts and "g2_decompress_only" in counts:
+            check_c = counts["per_set"]["sig_decode_subgroup"] - counts["g2_decompress_only"]
+            stage_counts["sig_decode_subgroup"] = counts["g2_decompress_only"] + (1.0 - share) * check_c
         for k, ms in stage_ms.items():
             if ms <= 0:
                 continue
@@ -502,6 +525,9 @@ def main():
                 "miller_lines": ({"active": True, "kernel_name": "k_lines", "fpmul_per_set": counts["per_set_lines"]["miller_lines"],
                                   "note": "untimed step on the hash stream between hash_to_g2 and miller_loop"}
                                  if counts and lines_active(n_sets) and "per_set_lines" in counts else {"active": False}),
+                "deferred_subgroup_checks": {"share_of_sets": share, "kernel_name": "k_sig_split",
+                                             "fpmul_per_set": round(share * check_c, 1) if check_c is not None else None,
+                                             "note": "untimed: beside the Miller loops, before the fold"},
                 "step_fpmul_G_per_s": round(counts["per_set_total"] * n_sets / (ms_per_step * 1e-3) / 1e9, 3) if counts else None}
 
     if rank == 0:
