@@ -103,36 +103,6 @@ def fpmul_counts():
     return json.load(open(p)) if os.path.exists(p) else None
 
 
-def lines_active(n_sets):
-    """Mirrors prepare() in bgv_api.hip: the one-lane Miller loop runs over
-    fixed-argument lines (BGV_LINES) when its items hold two pairs
-    (>= 65,536 sets unless BGV_PAIRS forces one); the lines are an untimed
-    step between the hash and Miller stages."""
-    e = os.environ.get("BGV_LINES")
-    if e is not None and e != "":
-        return e != "0" and n_sets >= 35000
-    p = os.environ.get("BGV_PAIRS")
-    return p == "2" or (p != "1" and n_sets >= 65536)
-
-
-def defer_share(n_sets):
-    """Mirrors prepare() in bgv_api.hip: the share of the sets whose G2
-    subgroup check leaves the signature stage for the SIMDs beside the Miller
-    loops (k_sig_split, untimed): half at two pairs per item, all between
-    35,000 and 65,535 sets, none below (latency mode)."""
-    if n_sets < 35000:
-        return 0.0
-    e = os.environ.get("BGV_DEFER_PCT")
-    if e:
-        return min(max(int(e), 0), 100) / 100.0
-    g = os.environ.get("BGV_DEFER_GRP")
-    p = os.environ.get("BGV_PAIRS")
-    two = p == "2" or (p != "1" and n_sets >= 65536)
-    if g:
-        return (0.5 if two else 1.0) if g != "0" else 0.0
-    return 0.5 if two else 1.0
-
-
 # stage -> its main kernel (rocprofv3 name) for the PMC traffic lookup
 STAGE_KERNEL = {"sig_decode_subgroup": "k_sig", "hash_to_g2": "k_hash", "pk_gather": "k_pk_chunk",
                 "pk_aggregate_scale": "k_pk", "sig_scale": "k_msm_bucket", "sig_sum_tree": "k_msm_job",
@@ -366,6 +336,49 @@ def shard_projection(d, torch, dev, arrays_host: dict, worlds=(2, 4, 8), reps: i
     return out
 
 
+def timed_steps(step, dist, coll_dev, torch, steps: int, warmup: int):
+    """W untimed + K timed steps between barriers; the max elapsed over ranks"""
+    for _ in range(warmup):
+        assert step(), "warm-up batch did not verify"
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ok = True
+    for _ in range(steps):
+        ok &= step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=coll_dev if coll_dev is not None else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, ok
+
+
+def weak_leg(d, torch, dev, dist, coll_dev, rank, world, args):
+    """N > 1 extra: every rank verifies its OWN whole segment (seeded per rank),
+    one 576-B partial per rank all-gathered, ONE final exponentiation; the
+    node's sets/s over all ranks (weak scaling, not BASELINE configs[3])."""
+    from lodestar_amd.dist import verify_sharded
+    seg = build_segment(list(range(args.blocks)), seed=SEED + 7919 * (rank + 1))
+    da = to_device(seg, torch, dev)
+    sigs = torch.zeros((seg["n_sets"], 192), dtype=torch.uint8, device=dev)
+    d.gen_sign(da, sigs, on_device=True)
+    da.update(sigs=sigs, sig_len=torch.full((seg["n_sets"],), 96, dtype=torch.int32, device=dev), scalars=None)
+
+    def step():
+        valid, jr = verify_sharded(d, da, dist, device=coll_dev, on_device=True)
+        return valid and bool((jr == 1).all())
+
+    elapsed, ok = timed_steps(step, dist, coll_dev, torch, args.steps, max(args.warmup, 1))
+    return {"sets_per_s": round(seg["n_sets"] * world * args.steps / elapsed, 1), "sets_per_rank": seg["n_sets"],
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "verified": ok,
+            "note": "every rank its own 32-epoch segment; one partial per rank all-gathered, one final exponentiation"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -374,8 +387,9 @@ def main():
     ap.add_argument("--blocks", type=int, default=1024, help="blocks in the segment (1024 = 32 epochs)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c2", action="store_true", help="skip the C1/C2/C3/C5, host-resident and shard legs (profiling runs)")
-    ap.add_argument("--shard", action="store_true",
-                    help="strong scaling: ONE segment split across the ranks by dist.shard_jobs (default: weak, one segment per rank)")
+    ap.add_argument("--weak", action="store_true",
+                    help="N > 1: every rank verifies its own segment (default: ONE segment split across the ranks, BASELINE configs[3])")
+    ap.add_argument("--no-weak-leg", action="store_true", help="N > 1: skip the extra weak-scaling measurement")
     args = ap.parse_args()
 
     import torch
@@ -397,20 +411,21 @@ def main():
     dev = torch.device("cuda", gpu)
     coll_dev = None if rehearse else dev  # where the collectives' tensors live
 
-    if args.shard:  # per-stage timing events also for shards below 65,536 sets
-        os.environ.setdefault("BGV_TIMING", "1")
+    shard = world > 1 and not args.weak
     from lodestar_amd import native
     from lodestar_amd.dist import gather_job_results, select_jobs, shard_jobs, verify_sharded
 
-    d = native.Device(gpu)
+    # per-stage timing events: automatic from 65,536 sets; forced for the
+    # smaller shards of N > 1 (they would add queue time to the N = 1 latency legs)
+    d = native.Device(gpu, timing=1) if world > 1 else native.Device(gpu)
     t0 = time.time()
     d.gen_keys(0, N_VALIDATORS, SEED)
     log(f"[bench] {N_VALIDATORS} keys generated in {time.time() - t0:.1f}s")
 
-    seg = build_segment(list(range(args.blocks)), seed=SEED + (0 if args.shard else rank))
+    seg = build_segment(list(range(args.blocks)), seed=SEED + (0 if shard else rank))
     jo = seg["job_offsets"]
-    shards = shard_jobs([int(jo[j + 1] - jo[j]) for j in range(seg["n_jobs"])], world) if args.shard else None
-    arrays = select_jobs(seg, shards[rank]) if args.shard else seg
+    shards = shard_jobs([int(jo[j + 1] - jo[j]) for j in range(seg["n_jobs"])], world) if shard else None
+    arrays = select_jobs(seg, shards[rank]) if shard else seg
     darr = to_device(arrays, torch, dev)
     n_sets = arrays["n_sets"]
     sigs = torch.zeros((n_sets, 192), dtype=torch.uint8, device=dev)
@@ -427,7 +442,7 @@ def main():
             jr, _ = d.verify(darr, on_device=True, want_set_codes=False)
             return bool((jr == 1).all())
         valid, local_jr = verify_sharded(d, darr, dist, device=coll_dev, on_device=True)
-        if args.shard:  # every rank ends with the whole segment's per-block verdicts
+        if shard:  # every rank ends with the whole segment's per-block verdicts
             full = gather_job_results(local_jr, shards, seg["n_jobs"], dist, device=coll_dev)
             return valid and bool((full == 1).all())
         return valid and bool((local_jr == 1).all())
@@ -457,14 +472,16 @@ def main():
         okt = torch.tensor([1 if all_ok else 0], device=coll_dev if coll_dev is not None else "cpu")
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         all_ok = bool(okt.item())
-    total_sets = seg["n_sets"] * (1 if args.shard else world)
+    total_sets = seg["n_sets"] * (1 if shard else world)
     ms_per_step = elapsed / args.steps * 1e3
     value = total_sets * args.steps / elapsed
 
     stage_ms = {d.stage_name(i): float(stage_sum[i] / args.steps) for i in range(native.N_STAGES) if d.stage_name(i) != "unknown"}
 
     legs = {}
-    if rank == 0 and not args.no_c2:
+    if shard and not args.no_weak_leg:
+        legs["weak_scaling"] = weak_leg(d, torch, dev, dist, coll_dev, rank, world, args)
+    if rank == 0 and world == 1 and not args.no_c2:
         legs.update(small_configs(d, torch, dev, arrays))
         host = dict(arrays)
         host["sigs"] = sigs.cpu().numpy()
@@ -487,9 +504,10 @@ def main():
         fpm_rate = 256 * 256 * 8 * 2048 / (fpm_ms * 1e-3) / 1e9
         per_stage = {}
         stage_counts = dict(counts["per_set"]) if counts else {}
-        if counts and lines_active(n_sets) and "per_set_lines" in counts:
+        lay = d.last_stats.layout()  # the variant the timed batches ran with (bgv_stats)
+        if counts and lay["lines"] and "per_set_lines" in counts:
             stage_counts["miller_loop"] = counts["per_set_lines"]["miller_loop"]
-        share = defer_share(n_sets)
+        share = (n_sets - min(lay["defer_from"], n_sets)) / max(n_sets, 1)
         check_c = None
         if counts and "g2_decompress_only" in counts:
             check_c = counts["per_set"]["sig_decode_subgroup"] - counts["g2_decompress_only"]
@@ -524,7 +542,8 @@ def main():
                 "per_stage": per_stage, "pubkey_gather": gather,
                 "miller_lines": ({"active": True, "kernel_name": "k_lines", "fpmul_per_set": counts["per_set_lines"]["miller_lines"],
                                   "note": "untimed step on the hash stream between hash_to_g2 and miller_loop"}
-                                 if counts and lines_active(n_sets) and "per_set_lines" in counts else {"active": False}),
+                                 if counts and lay["lines"] and "per_set_lines" in counts else {"active": False}),
+                "pipeline_variant": lay,
                 "deferred_subgroup_checks": {"share_of_sets": share, "kernel_name": "k_sig_split",
                                              "fpmul_per_set": round(share * check_c, 1) if check_c is not None else None,
                                              "note": "untimed: beside the Miller loops, before the fold"},
@@ -533,7 +552,7 @@ def main():
     if rank == 0:
         cpu = None if (args.no_cpu or world > 1) else cpu_baseline()
         par = (f"one segment sharded by job over {world} GPUs (shard_jobs), RCCL all-gather of Miller partials + per-job verdicts"
-               if args.shard else f"one segment per GPU x{world}, RCCL all-gather of Miller partials")
+               if shard else f"one segment per GPU x{world}, RCCL all-gather of Miller partials")
         out = {
             "metric": "BLS signature sets verified/sec (node)",
             "value": round(value, 1),
@@ -543,13 +562,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
-            "scaling": "strong" if args.shard else "weak",
+            "scaling": "weak" if args.weak else "strong",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (device-generated keys/signatures, seeded)",
             "config": {"workload": "C4 range-sync segment: 32 epochs = %d blocks x 98 sets (95 att k=128, sync k=512, 2 singles), 1M-validator table in HBM" % args.blocks,
-                       "sets": total_sets, "pubkey_refs": int(args.blocks * (ATT_PER_BLOCK * ATT_K + SYNC_K + 2)) * (1 if args.shard else world),
-                       "table_validators": N_VALIDATORS, "jobs": args.blocks * (1 if args.shard else world), "parallelism": par},
+                       "sets": total_sets, "pubkey_refs": int(args.blocks * (ATT_PER_BLOCK * ATT_K + SYNC_K + 2)) * (1 if shard else world),
+                       "table_validators": N_VALIDATORS, "jobs": args.blocks * (1 if shard else world), "parallelism": par},
             "c4_step_ms_p50": round(float(np.median(step_ms)), 3),
             **legs,
             "verified": all_ok,

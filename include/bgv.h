@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define BGV_ABI_VERSION 2
+#define BGV_ABI_VERSION 3
 
 /* ---- status of an API call (negative) ---------------------------------- */
 enum bgv_status {
@@ -139,7 +139,33 @@ typedef struct bgv_stats {
   uint32_t n_sets;
   uint32_t n_jobs;
   uint64_t pubkeys_aggregated;  /* lodestar_bls_aggregated_pubkeys_total */
+  /* the pipeline variant the batch ran with (chosen by batch size, or forced
+   * by bgv_cfg); also filled by bgv_last_stats                              */
+  uint32_t split;               /* 1: latency-mode hash and signature kernels */
+  uint32_t miller_lanes;        /* set-pair Miller loop: lanes per pair (1 = one-lane loop) */
+  uint32_t pairs_per_item;      /* one-lane loop: pairs sharing an accumulator */
+  uint32_t msm;                 /* 1: per-job bucket MSM for sum r_i sigma_i */
+  uint32_t lines;               /* 1: fixed-argument Miller lines */
+  uint32_t defer_from;          /* subgroup checks of sets >= defer_from run beside the Miller loops (n_sets: none) */
 } bgv_stats;
+
+/* Pipeline overrides for tests and A/B tools.  Production opens contexts with
+ * bgv_open (every field "auto": the variant is chosen per batch by its size,
+ * from measured sweeps).  No environment variable changes the pipeline.    */
+typedef struct bgv_cfg {
+  uint32_t struct_size; /* sizeof(bgv_cfg) */
+  int32_t split;        /* -1 auto; 0 bulk kernels; 1 latency mode (two-lane hash maps, cooperative G2) */
+  int32_t miller;       /* -1 auto; 1 one-lane set-pair loop; 6 / 18 / 36 lanes per pair (cooperative) */
+  int32_t job_lanes;    /* 0 auto (36); 6 / 18 / 36: lanes of the per-job (-G1, S_job) pairs */
+  int32_t msm;          /* -1 auto; 0 per-set [r_i] sigma_i + tree; 1 per-job bucket MSM */
+  int32_t pairs;        /* 0 auto; 1 / 2 pairs per one-lane Miller work item */
+  int32_t prefold;      /* -1 auto; 0 / 1 two-level per-job Miller fold */
+  int32_t lines;        /* -1 auto; 0 / 1 fixed-argument lines (bulk mode, one-lane loop) */
+  int32_t defer_pct;    /* -1 auto; 0..100: share of the G2 subgroup checks run beside the Miller loops (bulk mode) */
+  int32_t timing;       /* -1 auto (batches >= 65,536 sets); 0 / 1 per-stage timing events */
+} bgv_cfg;
+/* every field "auto" */
+void bgv_cfg_default(bgv_cfg* cfg);
 
 int bgv_abi_version(void);
 const char* bgv_set_code_name(int code); /* "BLST_BAD_ENCODING", ... */
@@ -150,6 +176,8 @@ const char* bgv_last_error(void);        /* thread-local text of the last failur
  * verifier at node start; this is the GPU branch's constructor, replacing
  * `new BlsMultiThreadWorkerPool(opts, modules)`, multithread/index.ts:120). */
 int bgv_open(int device, bgv_ctx** out);
+/* bgv_open with pipeline overrides (tests, A/B tools); cfg may be NULL */
+int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out);
 /* BlsMultiThreadWorkerPool.close (multithread/index.ts:193-214) */
 int bgv_close(bgv_ctx* ctx);
 

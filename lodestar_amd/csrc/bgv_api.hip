@@ -62,20 +62,10 @@ struct dbuf {
 
 struct bgv_ctx {
   int device = 0;
-  int miller_mode = -1;  // BGV_MILLER=serial|coop|6|18|36 forces the set-pair Miller layout (A/B tests); -1 = by batch size
-  int job_lanes = 0;     // BGV_JOB_LANES=6|18|36: layout of the (-G1, S_job) pairs; 0 = default
-  int msm_mode = -1;     // BGV_MSM=0|1 forces the signature combination (A/B tests); -1 = by batch shape
-  bool overlap = true;    // BGV_OVERLAP=0 runs every stage on one stream (A/B tests)
-  int split = -1;         // BGV_SPLIT=0|1 forces the latency mode (A/B tests); -1 = by batch size
-  int prefold = -1;       // BGV_PREFOLD=0|1 forces the two-level job fold (A/B tests); -1 = by batch shape
-  int pairs = 0;          // BGV_PAIRS=1|2 forces sets per Miller work item (A/B tests); 0 = by batch size
-  int timing = -1;        // BGV_TIMING=0|1: per-stage timing events; -1 = only for batches >= 65,536 sets
-  int defer = -1;         // BGV_DEFER bits (A/B): 1 = sig_scale after hash, 2 = sig after hash, 4 = pk stream low priority
-  int use_lines = -1;     // BGV_LINES=0|1: fixed-argument Miller lines in the one-lane loop; -1 = with two pairs per item
-  int defer_pct = -1;     // BGV_DEFER_PCT=0..100: share of the sets whose subgroup check is deferred (A/B); -1 = by mode
-  int defer_grp = -1;     // BGV_DEFER_GRP=0|1: bulk-mode subgroup checks beside the Miller loops; -1 = on
+  bgv_cfg cfg;            // pipeline overrides (bgv_open_cfg; all "auto" from bgv_open)
   bool timed = true;      // the last run_stages recorded per-stage events
   int run_from = 0, run_to = 0;  // stage range of the last run_stages (bgv_last_stats)
+  dev_batch last_d = {};         // the last run_stages batch (its pipeline variant for bgv_stats)
   hipStream_t st = nullptr, st_hash = nullptr, st_pk = nullptr;
   hipEvent_t ev[ST_COUNT + 1] = {};   // ev[s] = start of stage s on its stream
   hipEvent_t ev_end[ST_COUNT] = {};   // end of stage s on its stream
@@ -165,38 +155,45 @@ const char* bgv_stage_name(int stage) {
   return (stage >= 0 && stage < ST_COUNT) ? names[stage] : "unknown";
 }
 
-int bgv_open(int device, bgv_ctx** out) {
+void bgv_cfg_default(bgv_cfg* cfg) {
+  if (!cfg) return;
+  memset(cfg, 0, sizeof *cfg);
+  cfg->struct_size = sizeof *cfg;
+  cfg->split = cfg->miller = cfg->msm = cfg->prefold = cfg->lines = cfg->defer_pct = cfg->timing = -1;
+  cfg->job_lanes = cfg->pairs = 0;
+}
+
+int bgv_open(int device, bgv_ctx** out) { return bgv_open_cfg(device, nullptr, out); }
+
+int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
   if (!out) return fail(BGV_E_INVALID_ARG, "out is NULL");
   *out = nullptr;
+  bgv_cfg k;
+  bgv_cfg_default(&k);
+  if (cfg) {
+    if (cfg->struct_size != sizeof k) return fail(BGV_E_INVALID_ARG, "bgv_cfg.struct_size %u, expected %zu", cfg->struct_size, sizeof k);
+    k = *cfg;
+    auto lanes_ok = [](int v) { return v == 6 || v == 18 || v == 36; };
+    if (k.miller != -1 && k.miller != 1 && !lanes_ok(k.miller)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.miller %d", k.miller);
+    if (k.job_lanes != 0 && !lanes_ok(k.job_lanes)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.job_lanes %d", k.job_lanes);
+    if (k.pairs < 0 || k.pairs > 2) return fail(BGV_E_INVALID_ARG, "bgv_cfg.pairs %d", k.pairs);
+    if (k.defer_pct < -1 || k.defer_pct > 100) return fail(BGV_E_INVALID_ARG, "bgv_cfg.defer_pct %d", k.defer_pct);
+  }
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(BGV_E_NO_DEVICE, "no HIP device visible");
   if (device < 0 || device >= n) return fail(BGV_E_NO_DEVICE, "device %d out of range (%d devices)", device, n);
   HIPCHK(hipSetDevice(device));
   bgv_ctx* c = new bgv_ctx();
   c->device = device;
-  // BGV_MILLER=serial | coop (36 lanes per pair) | 6 | 18 | 36
-  if (const char* m = getenv("BGV_MILLER"))
-    c->miller_mode = strcmp(m, "serial") == 0 ? 0 : (atoi(m) == 6 || atoi(m) == 18) ? atoi(m) : 36;
-  if (const char* m = getenv("BGV_JOB_LANES")) c->job_lanes = (atoi(m) == 6 || atoi(m) == 18) ? atoi(m) : 36;
-  if (const char* m = getenv("BGV_MSM")) c->msm_mode = strcmp(m, "0") != 0 ? 1 : 0;
-  if (const char* o = getenv("BGV_OVERLAP")) c->overlap = strcmp(o, "0") != 0;
-  if (const char* o = getenv("BGV_PAIRS")) c->pairs = atoi(o);
-  if (const char* o = getenv("BGV_SPLIT")) c->split = atoi(o) != 0 ? 1 : 0;
-  if (const char* o = getenv("BGV_PREFOLD")) c->prefold = atoi(o) != 0 ? 1 : 0;
-  if (const char* o = getenv("BGV_TIMING")) c->timing = atoi(o) != 0 ? 1 : 0;
-  if (const char* o = getenv("BGV_DEFER")) c->defer = atoi(o);
-  if (const char* o = getenv("BGV_DEFER_GRP")) c->defer_grp = atoi(o) != 0 ? 1 : 0;
-  if (const char* o = getenv("BGV_DEFER_PCT")) c->defer_pct = atoi(o) < 0 ? 0 : (atoi(o) > 100 ? 100 : atoi(o));
-  if (const char* o = getenv("BGV_LINES")) c->use_lines = atoi(o) != 0 ? 1 : 0;
+  c->cfg = k;
   // hash -> set-pair Miller is the critical path: its stream (and the pubkey
   // stream feeding it) get the highest priority, signature decode/scaling the
   // lowest (it only feeds the signature tree and the 1 pair per job)
   int prio_lo = 0, prio_hi = 0;
   HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-  if (const char* p = getenv("BGV_PRIO")) if (strcmp(p, "0") == 0) prio_hi = prio_lo;
   HIPCHK(hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, prio_lo));
   HIPCHK(hipStreamCreateWithPriority(&c->st_hash, hipStreamNonBlocking, prio_hi));
-  HIPCHK(hipStreamCreateWithPriority(&c->st_pk, hipStreamNonBlocking, (c->defer > 0 && (c->defer & 4)) ? prio_lo : prio_hi));
+  HIPCHK(hipStreamCreateWithPriority(&c->st_pk, hipStreamNonBlocking, prio_hi));
   for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
   for (auto& e : c->ev_end) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipEventCreate(&c->ev_fork));
@@ -476,44 +473,37 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   //    (25,088 sets: 24.5 ms split against 26.3 ms; 50,176: 35.4 against 29.3);
   //  * two pairs per Miller work item only when the batch alone fills the chip.
   static const uint32_t MILLER_COOP_MAX = 6000, SPLIT_MAX = 35000, PAIRS2_MIN = 65536;
-  d.pairs_per_item = n >= PAIRS2_MIN ? 2 : 1;
-  if (c->pairs == 1 || c->pairs == 2) d.pairs_per_item = (uint32_t)c->pairs;
-  d.split = c->split >= 0 ? (uint32_t)c->split : (n < SPLIT_MAX ? 1u : 0u);
-  // bulk mode: decode in phase 1, subgroup checks beside the Miller loops
-  // (bgv_kernels.hip k_job_recode); the latency mode has its own split
-  // (one pair per Miller item: C4/2 28.3 -> 26.4 ms; with two pairs per item
-  // the checks slow the longer Miller phase more than they save: C4 40.4 -> 41.9)
-  d.defer_grp = c->defer_grp >= 0 ? (uint32_t)(!d.split && c->defer_grp)
-                                  : ((!d.split && d.pairs_per_item == 1) ? 1u : 0u);
-  // partial deferral: the checks of sets [defer_from, n) only (a multiple of
-  // 64).  With two pairs per item the Miller kernel leaves 240 SIMDs to the
-  // MSM tail and the job pairs; half of the checks fill them without
-  // outlasting it (C4, 3 runs each: none 39.75, 50% 39.27, 65% 39.31,
-  // all 39.89 ms)
-  d.defer_from = 0;
-  const int pct = c->defer_pct >= 0 ? c->defer_pct : (c->defer_grp < 0 && d.pairs_per_item == 2 ? 50 : -1);
-  if (pct >= 0 && !d.split) {
-    d.defer_grp = pct > 0 ? 1u : 0u;
-    d.defer_from = (uint32_t)(((uint64_t)n * (uint32_t)(100 - pct) / 100u) & ~63ull);
-  }
+  const bgv_cfg& k = c->cfg;
+  d.pairs_per_item = k.pairs ? (uint32_t)k.pairs : (n >= PAIRS2_MIN ? 2u : 1u);
+  d.split = k.split >= 0 ? (uint32_t)k.split : (n < SPLIT_MAX ? 1u : 0u);
+  // Deferred subgroup checks (bulk mode): the signature stage decodes, and the
+  // checks of sets [defer_from, n) run beside the Miller loops
+  // (bgv_kernels.hip k_job_recode).  All of them with one pair per Miller item
+  // (C4/2 28.3 -> 26.4 ms); half with two pairs per item: the Miller kernel
+  // leaves 240 SIMDs to the MSM tail and the job pairs, and half of the checks
+  // fill them without outlasting it (C4, 3 runs each: none 39.75, 50% 39.27,
+  // 65% 39.31, all 39.89 ms).  defer_from is a multiple of 64 (wave-uniform).
+  const int pct = d.split ? 0 : (k.defer_pct >= 0 ? k.defer_pct : (d.pairs_per_item == 2 ? 50 : 100));
+  d.defer_grp = pct > 0 ? 1u : 0u;
+  d.defer_from = pct > 0 ? (uint32_t)(((uint64_t)n * (uint32_t)(100 - pct) / 100u) & ~63ull) : n;
   // two-level per-job fold (bgv_tail.hip) when few jobs of >= 64 sets leave
   // the chip idle: groups of ~sqrt(span) sets fold side by side, then the job
   // folds the group values, 2 sqrt(span) sequential Fp12 products instead of span
   {
     const bool few_big = d.n_jobs <= 256 && d.span_log2 >= 6 && d.span_log2 <= 8;
-    const bool on = c->prefold >= 0 ? (c->prefold && d.span_log2 >= 2 && d.span_log2 <= 8) : few_big;
+    const bool on = k.prefold >= 0 ? (k.prefold && d.span_log2 >= 2 && d.span_log2 <= 8) : few_big;
     d.prefold_log2 = on ? (d.span_log2 + 1) / 2 : 0u;
   }
-  d.miller_coop = c->miller_mode >= 0 ? (uint32_t)c->miller_mode : (n < MILLER_COOP_MAX ? 36u : 0u);
+  d.miller_coop = k.miller >= 0 ? (k.miller == 1 ? 0u : (uint32_t)k.miller) : (n < MILLER_COOP_MAX ? 36u : 0u);
   // fixed-argument lines (pairing.h miller_lines): the G2 half of the one-lane
   // Miller loop moves to the hash stream, phase 1 (C4 40.4 -> 39.5 ms); with
   // one pair per item it loses (C4/2 26.4 -> 28.5 ms)
-  d.lines = (uint32_t)(!d.split && !d.miller_coop && (c->use_lines >= 0 ? c->use_lines : d.pairs_per_item == 2));
-  d.job_lanes = c->job_lanes ? (uint32_t)c->job_lanes : 36u;
+  d.lines = (uint32_t)(!d.split && !d.miller_coop && (k.lines >= 0 ? k.lines : d.pairs_per_item == 2));
+  d.job_lanes = k.job_lanes ? (uint32_t)k.job_lanes : 36u;
   // sum r_i sigma_i per job by a bucket MSM (16 x 4-bit windows, ~1,800 G2
   // additions per 98-set job instead of 98 x 75 in per-set scalar mults)
   // when jobs are block-sized (<= 256 sets)
-  d.msm = c->msm_mode >= 0 ? (uint32_t)c->msm_mode : ((n >= MILLER_COOP_MAX && d.span_log2 <= 8) ? 1u : 0u);
+  d.msm = k.msm >= 0 ? (uint32_t)k.msm : ((n >= MILLER_COOP_MAX && d.span_log2 <= 8) ? 1u : 0u);
   if (b->scalars && !b->on_device) {
     // staged with the other host arrays above
   } else if (b->scalars) {
@@ -586,9 +576,10 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
 // the critical path, so latency batches record only the stream dependencies
 // (untimed events) and the total.
 static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int from, int to) {
-  const bool fork = c->overlap && from <= ST_SIG && to > ST_F_TREE;
-  const bool timed = c->timing >= 0 ? c->timing != 0 : d.n_sets >= 65536;
+  const bool fork = from <= ST_SIG && to > ST_F_TREE;
+  const bool timed = c->cfg.timing >= 0 ? c->cfg.timing != 0 : d.n_sets >= 65536;
   c->timed = timed;
+  c->last_d = d;
   c->run_from = from;
   c->run_to = to;
   hipEvent_t* dep = timed ? c->ev_end : c->ev_dep;  // what the stream waits below wait on
@@ -597,7 +588,6 @@ static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int fro
   // only the messages and heads the critical path (hash -> Miller -> fold ->
   // final exp); large batches keep the set-up alone on the GPU (its
   // one-workgroup scan starves under the bulk kernels)
-  const int defer = c->defer > 0 ? (c->defer & 3) : 0;
   const bool early_hash = fork && d.split && from <= ST_HASH && to > ST_HASH;
   auto launch_one = [&](int s) -> int {
     hipStream_t st = c->st;
@@ -612,8 +602,6 @@ static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int fro
       if (s == ST_PK || s == ST_PK_SCALE) st = c->st_pk;
       if (s == ST_S_TREE || s == ST_MILLER) HIPCHK(hipStreamWaitEvent(st, dep[ST_PK_SCALE], 0));
       if (s == ST_F_TREE) HIPCHK(hipStreamWaitEvent(st, dep[ST_MILLER], 0));
-      if (defer && ((s == ST_SIG_SCALE && (defer & 1)) || (s == ST_SIG && (defer & 2))))
-        HIPCHK(hipStreamWaitEvent(st, dep[ST_HASH], 0));
     }
     if (timed) HIPCHK(hipEventRecord(c->ev[s], st));
     // deferred subgroup checks: their verdicts enter the codes before the fold
@@ -650,16 +638,20 @@ static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int fro
     if (!early_hash) HIPCHK(hipStreamWaitEvent(c->st_hash, c->ev_prep, 0));
     HIPCHK(hipStreamWaitEvent(c->st_pk, c->ev_prep, 0));
   }
-  int order[ST_COUNT], n_order = 0;
-  // deferred signature work waits on the hash's event: the hash is enqueued first
-  const bool hash_first = !early_hash && fork && defer && from <= ST_HASH && to > ST_HASH;
-  if (hash_first) order[n_order++] = ST_HASH;
   for (int s = from; s < to; s++)
-    if (!((early_hash || hash_first) && s == ST_HASH)) order[n_order++] = s;
-  for (int oi = 0; oi < n_order; oi++)
-    if (int r = launch_one(order[oi])) return r;
+    if (!(early_hash && s == ST_HASH))
+      if (int r = launch_one(s)) return r;
   HIPCHK(hipEventRecord(c->ev[to], c->st));
   return 0;
+}
+
+static void stats_layout(bgv_stats* s, const dev_batch& d) {
+  s->split = d.split;
+  s->miller_lanes = d.miller_coop ? d.miller_coop : 1u;
+  s->pairs_per_item = d.pairs_per_item;
+  s->msm = d.msm;
+  s->lines = d.lines;
+  s->defer_from = d.defer_grp ? d.defer_from : d.n_sets;
 }
 
 // job results, set codes and the batch flag through pinned memory; the
@@ -685,6 +677,7 @@ static int finish_results(bgv_ctx* c, const dev_batch& d, const dev_work& w, int
     HIPCHK(hipEventElapsedTime(&stats->total_ms, c->ev[0], c->ev[ST_COUNT]));
     stats->n_sets = d.n_sets;
     stats->n_jobs = d.n_jobs;
+    stats_layout(stats, d);
     uint32_t valid_jobs = 0, valid_sets = 0;
     const uint32_t* jo = c->jo_host.data();
     for (uint32_t j = 0; j < d.n_jobs; j++)
@@ -705,6 +698,7 @@ int bgv_last_stats(bgv_ctx* c, bgv_stats* stats) {
   if (c->timed)
     for (int s = c->run_from; s < c->run_to && s < BGV_N_STAGES; s++) HIPCHK(hipEventElapsedTime(&stats->stage_ms[s], c->ev[s], c->ev_end[s]));
   HIPCHK(hipEventElapsedTime(&stats->total_ms, c->ev[c->run_from], c->ev[c->run_to]));
+  stats_layout(stats, c->last_d);
   return BGV_OK;
 }
 

@@ -25,7 +25,7 @@ BGV_E_TABLE_RANGE = -4
 BGV_E_EMPTY_SET = -5
 BGV_E_BAD_PUBKEY = -6
 BGV_E_STATE = -7
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 SET_CODE_NAMES = {
     0: "BLST_SUCCESS",
@@ -46,7 +46,8 @@ PK_UNCOMPRESSED_96 = 1
 N_STAGES = 16
 
 EXPORTS = [
-    "bgv_abi_version", "bgv_set_code_name", "bgv_stage_name", "bgv_last_error", "bgv_open", "bgv_close",
+    "bgv_abi_version", "bgv_set_code_name", "bgv_stage_name", "bgv_last_error", "bgv_open", "bgv_open_cfg",
+    "bgv_cfg_default", "bgv_close",
     "bgv_pubkeys_set", "bgv_pubkeys_count", "bgv_pubkeys_get", "bgv_pubkeys_validate", "bgv_verify", "bgv_last_stats",
     "bgv_partial", "bgv_partial_finish", "bgv_combine_final", "bgv_debug_stages", "bgv_gen_keys", "bgv_gen_sign", "bgv_bench_fpmul",
     "bgv_bench_mad", "bgv_debug_fp_ops",
@@ -86,7 +87,14 @@ class BgvStats(ctypes.Structure):
         ("n_sets", ctypes.c_uint32),
         ("n_jobs", ctypes.c_uint32),
         ("pubkeys_aggregated", ctypes.c_uint64),
+        ("split", ctypes.c_uint32),
+        ("miller_lanes", ctypes.c_uint32),
+        ("pairs_per_item", ctypes.c_uint32),
+        ("msm", ctypes.c_uint32),
+        ("lines", ctypes.c_uint32),
+        ("defer_from", ctypes.c_uint32),
     ]
+    LAYOUT = ("split", "miller_lanes", "pairs_per_item", "msm", "lines", "defer_from")
 
     def as_dict(self, lib=None):
         names = [lib.stage_name(i) for i in range(N_STAGES)] if lib else [str(i) for i in range(N_STAGES)]
@@ -98,7 +106,30 @@ class BgvStats(ctypes.Structure):
             "n_sets": int(self.n_sets),
             "n_jobs": int(self.n_jobs),
             "pubkeys_aggregated": int(self.pubkeys_aggregated),
+            "layout": self.layout(),
         }
+
+    def layout(self) -> dict:
+        """the pipeline variant the last batch ran with (prepare() in bgv_api.hip)"""
+        return {k: int(getattr(self, k)) for k in self.LAYOUT}
+
+
+class BgvCfg(ctypes.Structure):
+    """bgv_cfg (include/bgv.h): pipeline overrides for tests and A/B tools.
+    Production contexts use the defaults (every field "auto")."""
+    _fields_ = [("struct_size", ctypes.c_uint32)] + [
+        (k, ctypes.c_int32) for k in
+        ("split", "miller", "job_lanes", "msm", "pairs", "prefold", "lines", "defer_pct", "timing")]
+    AUTO = {"split": -1, "miller": -1, "job_lanes": 0, "msm": -1, "pairs": 0, "prefold": -1, "lines": -1,
+            "defer_pct": -1, "timing": -1}
+
+    @classmethod
+    def make(cls, **over) -> "BgvCfg":
+        bad = set(over) - set(cls.AUTO)
+        if bad:
+            raise ValueError(f"unknown bgv_cfg fields {sorted(bad)}")
+        c = cls(struct_size=ctypes.sizeof(cls), **{**cls.AUTO, **over})
+        return c
 
 
 class BgvDebug(ctypes.Structure):
@@ -128,6 +159,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
             "bgv_stage_name": ([ctypes.c_int], ctypes.c_char_p),
             "bgv_last_error": ([], ctypes.c_char_p),
             "bgv_open": ([ctypes.c_int, ctypes.POINTER(P)], ctypes.c_int),
+            "bgv_open_cfg": ([ctypes.c_int, ctypes.POINTER(BgvCfg), ctypes.POINTER(P)], ctypes.c_int),
+            "bgv_cfg_default": ([ctypes.POINTER(BgvCfg)], None),
             "bgv_close": ([P], ctypes.c_int),
             "bgv_pubkeys_set": ([P, u32, u32, P, u32], ctypes.c_int),
             "bgv_pubkeys_count": ([P, ctypes.POINTER(u32)], ctypes.c_int),
@@ -167,10 +200,14 @@ def _ptr(a) -> int | None:
 class Device:
     """One bgv_ctx: a HIP device, its stream and its HBM pubkey table."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, **cfg):
+        """cfg: bgv_cfg overrides (tests and A/B tools only), e.g. miller=36, split=0"""
         self.lib = load_library()
         h = ctypes.c_void_p()
-        self._check(self.lib.bgv_open(device, ctypes.byref(h)))
+        if cfg:
+            self._check(self.lib.bgv_open_cfg(device, ctypes.byref(BgvCfg.make(**cfg)), ctypes.byref(h)))
+        else:
+            self._check(self.lib.bgv_open(device, ctypes.byref(h)))
         self.h = h
         self.device = device
         self.last_stats = BgvStats()

@@ -22,7 +22,7 @@ def lib():
 
 def declared_functions():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(bgv_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(bgv_\w+)\s*\(", src, re.M)))
 
 
 def test_every_declared_symbol_is_exported(lib):
@@ -41,14 +41,17 @@ def test_struct_layout_matches_ctypes(tmp_path):
     fields_b = [f for f, _ in native.BgvBatch._fields_]
     fields_s = [f for f, _ in native.BgvStats._fields_]
     fields_d = [f for f, _ in native.BgvDebug._fields_]
+    fields_c = [f for f, _ in native.BgvCfg._fields_]
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "bgv.h"', "int main(void){"]
-    lines.append('printf("%zu %zu %zu\\n", sizeof(bgv_batch), sizeof(bgv_stats), sizeof(bgv_debug));')
+    lines.append('printf("%zu %zu %zu %zu\\n", sizeof(bgv_batch), sizeof(bgv_stats), sizeof(bgv_debug), sizeof(bgv_cfg));')
     for f in fields_b:
         lines.append(f'printf("%zu\\n", offsetof(bgv_batch, {f}));')
     for f in fields_s:
         lines.append(f'printf("%zu\\n", offsetof(bgv_stats, {f}));')
     for f in fields_d:
         lines.append(f'printf("%zu\\n", offsetof(bgv_debug, {f}));')
+    for f in fields_c:
+        lines.append(f'printf("%zu\\n", offsetof(bgv_cfg, {f}));')
     lines.append("return 0;}")
     c.write_text("\n".join(lines))
     exe = tmp_path / "layout"
@@ -57,16 +60,18 @@ def test_struct_layout_matches_ctypes(tmp_path):
     assert int(vals[0]) == ctypes.sizeof(native.BgvBatch)
     assert int(vals[1]) == ctypes.sizeof(native.BgvStats)
     assert int(vals[2]) == ctypes.sizeof(native.BgvDebug)
-    offs = [int(v) for v in vals[3:]]
-    nb, ns = len(fields_b), len(fields_s)
+    assert int(vals[3]) == ctypes.sizeof(native.BgvCfg)
+    offs = [int(v) for v in vals[4:]]
+    nb, ns, nd = len(fields_b), len(fields_s), len(fields_d)
     assert offs[:nb] == [getattr(native.BgvBatch, f).offset for f in fields_b]
     assert offs[nb:nb + ns] == [getattr(native.BgvStats, f).offset for f in fields_s]
-    assert offs[nb + ns:] == [getattr(native.BgvDebug, f).offset for f in fields_d]
+    assert offs[nb + ns:nb + ns + nd] == [getattr(native.BgvDebug, f).offset for f in fields_d]
+    assert offs[nb + ns + nd:] == [getattr(native.BgvCfg, f).offset for f in fields_c]
 
 
 def test_metadata_and_no_silent_fallback(lib):
     from lodestar_amd import native
-    assert lib.bgv_abi_version() == native.ABI_VERSION == 2
+    assert lib.bgv_abi_version() == native.ABI_VERSION == 3
     assert lib.bgv_set_code_name(8) == b"BLST_INVALID_SIZE"
     assert lib.bgv_set_code_name(3) == b"BLST_POINT_NOT_IN_GROUP"
     assert lib.bgv_stage_name(6) == b"miller_loop"
@@ -85,3 +90,31 @@ def test_metadata_and_no_silent_fallback(lib):
 def test_gfx950_code_object_present(lib):
     blob = open(os.path.join(ROOT, "lodestar_amd", "libbgv.so"), "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob  # the fat binary carries a gfx950 code object
+
+
+def test_no_environment_steers_the_pipeline(lib):
+    """The pipeline variant is chosen per batch (prepare()) or forced by an
+    explicit bgv_cfg; the library reads no environment variable."""
+    out = subprocess.check_output(["nm", "-D", "--undefined-only", os.path.join(ROOT, "lodestar_amd", "libbgv.so")]).decode()
+    assert "getenv" not in out
+    src = "".join(open(os.path.join(ROOT, "lodestar_amd", "csrc", f)).read()
+                  for f in os.listdir(os.path.join(ROOT, "lodestar_amd", "csrc")))
+    assert "getenv" not in src
+
+
+def test_cfg_defaults_and_validation(lib):
+    from lodestar_amd import native
+    c = native.BgvCfg()
+    lib.bgv_cfg_default(ctypes.byref(c))
+    assert c.struct_size == ctypes.sizeof(native.BgvCfg)
+    assert {k: getattr(c, k) for k in native.BgvCfg.AUTO} == native.BgvCfg.AUTO
+    h = ctypes.c_void_p()
+    # invalid overrides are refused before any device call (no GPU needed)
+    for bad in ({"miller": 7}, {"job_lanes": 5}, {"pairs": 3}, {"defer_pct": 101}):
+        st = lib.bgv_open_cfg(0, ctypes.byref(native.BgvCfg.make(**bad)), ctypes.byref(h))
+        assert st == native.BGV_E_INVALID_ARG, bad
+    c2 = native.BgvCfg.make()
+    c2.struct_size = 4
+    assert lib.bgv_open_cfg(0, ctypes.byref(c2), ctypes.byref(h)) == native.BGV_E_INVALID_ARG
+    with pytest.raises(ValueError):
+        native.BgvCfg.make(overlap=0)

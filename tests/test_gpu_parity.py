@@ -219,15 +219,14 @@ def test_microbench_runs(dev):
     assert dev.bench_mad(256 * 64, 64) > 0
 
 
-def test_cooperative_miller_bit_identical_to_serial(monkeypatch):
+def test_cooperative_miller_bit_identical_to_serial():
     """The cooperative Miller loop (miller_coop.h) in its three layouts (36,
-    6 and 18 lanes per pair) and the one-lane loop (pairing.h, BGV_MILLER=serial)
+    6 and 18 lanes per pair) and the one-lane loop (pairing.h, bgv_cfg.miller = 1)
     produce the same Fp12 batch partial, byte for byte, and the same verdicts."""
     from lodestar_amd import native
     outs = {}
     for mode in ("serial", "coop", "6", "18"):
-        monkeypatch.setenv("BGV_MILLER", mode)
-        d = native.Device(0)
+        d = native.Device(0, miller={"serial": 1, "coop": 36, "6": 6, "18": 18}[mode])
         try:
             G.load_golden_table(d)
             a, expected, _ = G.golden_arrays([0, 1, 9, 11, 12, 13], scalars_seed=3)
@@ -336,7 +335,7 @@ def test_single_set_and_light_client_aggregate():
         asyncio.run(pool.close())
 
 
-def test_signature_msm_bit_identical_to_per_set_scaling(monkeypatch):
+def test_signature_msm_bit_identical_to_per_set_scaling():
     """sum_j r_i sigma_i by the per-job bucket MSM (k_msm_*, default for
     large batches) and by per-set [r_i] sigma_i + tree give the same S_job:
     the batch partial (which holds the (-G1, S_job) Miller values) is
@@ -344,8 +343,7 @@ def test_signature_msm_bit_identical_to_per_set_scaling(monkeypatch):
     from lodestar_amd import native
     outs = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("BGV_MSM", mode)
-        d = native.Device(0)
+        d = native.Device(0, msm=int(mode))
         try:
             G.load_golden_table(d)
             a, _, _ = G.golden_arrays([0, 1, 9, 10, 11, 12, 13], scalars_seed=5)
@@ -368,17 +366,16 @@ def test_signature_msm_bit_identical_to_per_set_scaling(monkeypatch):
 
 
 @pytest.mark.gpu
-def test_latency_split_mode_bit_identical(monkeypatch):
-    """Latency mode (BGV_SPLIT=1, default below 65,536 sets: two map lanes
+def test_latency_split_mode_bit_identical():
+    """Latency mode (bgv_cfg.split = 1, default below 35,000 sets: two map lanes
     per message, subgroup check beside [r_i] sigma_i) and the one-lane-per-set
-    kernels (BGV_SPLIT=0) give the same batch partial, byte for byte, and the
+    kernels (split = 0) give the same batch partial, byte for byte, and the
     same per-job verdicts and set codes on the golden jobs (which include
     off-curve and out-of-subgroup signatures)."""
     from lodestar_amd import native
     outs = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("BGV_SPLIT", mode)
-        d = native.Device(0)
+        d = native.Device(0, split=int(mode))
         try:
             G.load_golden_table(d)
             a, expected, codes = G.golden_arrays([0, 1, 9, 11, 12, 13], scalars_seed=3)
@@ -399,10 +396,10 @@ def test_latency_split_mode_bit_identical(monkeypatch):
 
 
 @pytest.mark.gpu
-def test_two_level_job_fold_bit_identical(monkeypatch):
+def test_two_level_job_fold_bit_identical():
     """The two-level per-job fold (k_job_prefold, default for <= 256 jobs of
     >= 64 sets: groups of ~sqrt(span) sets fold side by side, then the job
-    folds the group values) and the one-level fold (BGV_PREFOLD=0) give the
+    folds the group values) and the one-level fold (bgv_cfg.prefold = 0) give the
     same batch partial, byte for byte, on ragged jobs (64, 100, 3, 1 and 132
     sets), the same per-job verdicts when the batch check fails and every job
     takes its own final exponentiation, and a passing batch when no set is
@@ -411,8 +408,7 @@ def test_two_level_job_fold_bit_identical(monkeypatch):
     offs = [0, 64, 164, 167, 168, 300]
     outs = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("BGV_PREFOLD", mode)
-        d = native.Device(0)
+        d = native.Device(0, prefold=int(mode))
         try:
             first = d.pubkeys_count()
             d.gen_keys(first, 256, 5)

@@ -26,10 +26,10 @@ pytestmark = pytest.mark.gpu
 
 MODES = {
     "latency": {},
-    "coop6_jobs18": {"BGV_MILLER": "6", "BGV_JOB_LANES": "18"},
-    "bulk": {"BGV_SPLIT": "0"},
-    "bulk_serial_msm": {"BGV_SPLIT": "0", "BGV_MILLER": "serial", "BGV_MSM": "1", "BGV_PAIRS": "1"},
-    "c4_path": {"BGV_SPLIT": "0", "BGV_MILLER": "serial", "BGV_MSM": "1", "BGV_PAIRS": "2"},
+    "coop6_jobs18": {"miller": 6, "job_lanes": 18},
+    "bulk": {"split": 0},
+    "bulk_serial_msm": {"split": 0, "miller": 1, "msm": 1, "pairs": 1},
+    "c4_path": {"split": 0, "miller": 1, "msm": 1, "pairs": 2},
 }
 
 
@@ -49,12 +49,10 @@ def golden():
 
 
 @pytest.mark.parametrize("mode", list(MODES))
-def test_stage_values_match_oracle(monkeypatch, golden, mode):
+def test_stage_values_match_oracle(golden, mode):
     from lodestar_amd import native
     v, sets = golden
-    for k, val in MODES[mode].items():
-        monkeypatch.setenv(k, val)
-    d = native.Device(0)
+    d = native.Device(0, **MODES[mode])
     try:
         G.load_golden_table(d)
         arrays, expected, codes = G.golden_arrays()
@@ -77,7 +75,7 @@ def test_stage_values_match_oracle(monkeypatch, golden, mode):
     # set pairs: one Miller value per set, or (two pairs per work item) the
     # item's product at its first set and the identity at its second; an item
     # with a rejected pubkey contributes the identity
-    pairs = MODES[mode].get("BGV_PAIRS", "1") == "2"
+    pairs = MODES[mode].get("pairs", 1) == 2
     jo = arrays["job_offsets"]
     for j in range(J):
         beg, end = int(jo[j]), int(jo[j + 1])

@@ -33,7 +33,7 @@ def test_addon_loads_and_exports():
 const a = require({addon!r});
 const want = ["abiVersion","codeName","open","close","pubkeysSet","pubkeysCount","pubkeysValidate","verify","verifySync"];
 for (const k of want) if (typeof a[k] !== "function") throw Error("missing " + k);
-if (a.abiVersion() !== 2) throw Error("abi " + a.abiVersion());
+if (a.abiVersion() !== 3) throw Error("abi " + a.abiVersion());
 if (a.codeName(8) !== "BLST_INVALID_SIZE" || a.codeName(3) !== "BLST_POINT_NOT_IN_GROUP") throw Error("names");
 // without a GPU open() throws a bgv error; with one it yields a working context
 let ctx = null;

@@ -1,7 +1,8 @@
 """A/B sweep of the pipeline knobs over batch sizes (one GPU): for each
-(size, knob set) the median on-device bgv_verify time of a C4-shaped batch
-(the first `size` sets' whole blocks of the segment).  Prints one JSON line
-per point.  Knobs are read by bgv_open, so every point opens its own context.
+(size, bgv_cfg override set) the median on-device bgv_verify time of a
+C4-shaped batch (the first `size` sets' whole blocks of the segment).  Prints
+one JSON line per point.  Every override set opens its own context
+(bgv_open_cfg).
 
     python tools/sweep_modes.py [--sizes 12544,25088,50176,100352] [--reps 5]
 """
@@ -16,33 +17,25 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-MODES = {
+MODES = {  # bgv_cfg overrides (include/bgv.h)
     "default": {},
-    "split0": {"BGV_SPLIT": "0"},
-    "split0_serial": {"BGV_SPLIT": "0", "BGV_MILLER": "serial"},
-    "split0_serial_msm": {"BGV_SPLIT": "0", "BGV_MILLER": "serial", "BGV_MSM": "1"},
-    "bulk_c4": {"BGV_SPLIT": "0", "BGV_MILLER": "serial", "BGV_MSM": "1", "BGV_PAIRS": "2"},
-    "split1_serial_msm": {"BGV_SPLIT": "1", "BGV_MILLER": "serial", "BGV_MSM": "1"},
-    "coop_msm": {"BGV_MSM": "1"},
-    "split1_serial": {"BGV_SPLIT": "1", "BGV_MILLER": "serial", "BGV_MSM": "0"},
-    "split1_coop_msm": {"BGV_SPLIT": "1", "BGV_MILLER": "coop", "BGV_MSM": "1"},
-    "m6": {"BGV_MILLER": "6"},
-    "m18": {"BGV_MILLER": "18"},
-    "m36": {"BGV_MILLER": "36"},
-    "serial": {"BGV_MILLER": "serial"},
-    "m6_s0": {"BGV_MILLER": "6", "BGV_SPLIT": "0"},
-    "j18": {"BGV_JOB_LANES": "18"},
-    "j6": {"BGV_JOB_LANES": "6"},
-    "isolated": {"BGV_OVERLAP": "0", "BGV_TIMING": "1"},
-    "d1": {"BGV_DEFER": "1"},
-    "d2": {"BGV_DEFER": "2"},
-    "d4": {"BGV_DEFER": "4"},
-    "d5": {"BGV_DEFER": "5"},
-    "d6": {"BGV_DEFER": "6"},
-    "noprio": {"BGV_PRIO": "0"},
+    "split0": {"split": 0},
+    "split0_serial": {"split": 0, "miller": 1},
+    "split0_serial_msm": {"split": 0, "miller": 1, "msm": 1},
+    "bulk_c4": {"split": 0, "miller": 1, "msm": 1, "pairs": 2},
+    "split1_serial_msm": {"split": 1, "miller": 1, "msm": 1},
+    "coop_msm": {"msm": 1},
+    "split1_serial": {"split": 1, "miller": 1, "msm": 0},
+    "split1_coop_msm": {"split": 1, "miller": 36, "msm": 1},
+    "m6": {"miller": 6},
+    "m18": {"miller": 18},
+    "m36": {"miller": 36},
+    "serial": {"miller": 1},
+    "m6_s0": {"miller": 6, "split": 0},
+    "j18": {"job_lanes": 18},
+    "j6": {"job_lanes": 6},
+    "timed": {"timing": 1},
 }
-KNOBS = ("BGV_SPLIT", "BGV_MILLER", "BGV_MSM", "BGV_PAIRS", "BGV_PREFOLD", "BGV_JOB_LANES", "BGV_OVERLAP", "BGV_TIMING",
-         "BGV_DEFER", "BGV_PRIO")
 
 
 def main():
@@ -72,10 +65,7 @@ def main():
         batches[n] = da
     signer.close()
     for name in args.modes.split(","):
-        for k in KNOBS:
-            os.environ.pop(k, None)
-        os.environ.update(MODES[name])
-        d = native.Device(0)
+        d = native.Device(0, **MODES[name])
         d.gen_keys(0, bench.N_VALIDATORS, bench.SEED)
         for n in sizes:
             da = batches[n]
@@ -89,7 +79,8 @@ def main():
                 t.append(time.perf_counter() - t1)
             ms = float(np.median(t)) * 1e3
             row = {"mode": name, "sets": n, "ms": round(ms, 3), "sets_per_s": round(n / ms * 1e3, 1)}
-            if os.environ.get("BGV_TIMING") == "1" or n >= 65536:  # per-stage event times of the last call
+            row["layout"] = d.last_stats.layout()
+            if MODES[name].get("timing") == 1 or n >= 65536:  # per-stage event times of the last call
                 row["stage_ms"] = {k: round(v, 3) for k, v in d.last_stats.as_dict(d)["stage_ms"].items() if v > 0}
             print(json.dumps(row), flush=True)
         d.close()
