@@ -11,6 +11,12 @@
  *   pubkeysValidate(ctx, Uint8Array) -> Int32Array   bgv_pubkeys_validate (processDeposit.ts:57-66)
  *   verify(ctx, batch) -> Promise<result>        bgv_verify on the libuv pool (worker.ts:30-106)
  *   verifySync(ctx, batch) -> result             verifyOnMainThread / BlsSingleThreadVerifier
+ *   partial(ctx, batch) -> Promise<result + {miller: Uint8Array(576), ok}>
+ *                                                bgv_partial: one shard of a multi-GPU batch
+ *   combineFinal(ctx, Uint8Array(576 n)) -> Promise<boolean>
+ *                                                bgv_combine_final: ONE final exponentiation of the shards
+ *   partialFinish(ctx) -> Promise<result>        bgv_partial_finish: localise the last partial()'s shard
+ *                                                after a failed combined check
  *
  * batch = {jobOffsets: Uint32Array, pkOffsets: Uint32Array, pkIndices:
  * Uint32Array, msgs: Uint8Array, sigs: Uint8Array (192 B per set), sigLen:
@@ -18,7 +24,12 @@
  * result = {results: Int32Array (bgv_job_result per job: 1 valid, 0 invalid,
  * -code rejected), batchRetries, batchSigsSuccess, pubkeysAggregated,
  * deviceMs, workerStartMs, workerEndMs}: the BlsWorkResult fields
- * (multithread/types.ts:26-38) the pool's metrics are fed from.
+ * (multithread/types.ts:26-38) the pool's metrics are fed from.  For
+ * partial() `results` is provisional: -code for a job rejected by a parse /
+ * subgroup / pubkey error (final), 1 for every other job (valid iff the
+ * combined check passes).  Contexts on different devices run their queued
+ * work concurrently on the libuv pool (one pool thread per call in flight:
+ * size UV_THREADPOOL_SIZE >= the device count, napi/index.js does).
  *
  * Ownership: the offset arrays are copied when the call
  * is made and every length is checked against the copies, so a caller that
@@ -49,6 +60,7 @@ typedef struct {
   bgv_ctx* ctx;
   pthread_mutex_t mu;
   int closed;
+  uint32_t partial_jobs; /* job count of the last partial() (sizes partialFinish's results) */
 } addon_ctx;
 
 static void ctx_finalize(napi_env env, void* data, void* hint) {
@@ -225,9 +237,16 @@ static const napi_typedarray_type FIELD_T[N_FIELDS] = {napi_uint32_array, napi_u
                                                        napi_uint8_array,  napi_uint8_array,  napi_uint32_array,
                                                        napi_uint8_array};
 
+enum { K_VERIFY, K_PARTIAL, K_FINISH, K_COMBINE };
+
 typedef struct {
+  int kind;
   addon_ctx* c;
   bgv_batch b;
+  uint8_t miller[576];  /* K_PARTIAL */
+  int32_t ok;           /* K_PARTIAL: no job rejected; K_COMBINE: the product is 1 in GT */
+  uint8_t* parts;       /* K_COMBINE: a copy of the partials */
+  uint32_t n_parts;
   uint32_t* job_off; /* copies made at call time (the library reads these) */
   uint32_t* pk_off;
   int32_t* job_result;
@@ -245,8 +264,10 @@ static void free_job_arrays(verify_job* j) {
   free(j->job_off);
   free(j->pk_off);
   free(j->job_result);
+  free(j->parts);
   j->job_off = j->pk_off = NULL;
   j->job_result = NULL;
+  j->parts = NULL;
 }
 
 /* reads the batch object into j->b; copies the offsets; pins the other arrays when pin != 0 */
@@ -321,7 +342,23 @@ static void run_verify(verify_job* j) {
     j->status = BGV_E_INVALID_ARG;
     snprintf(j->err, sizeof j->err, "QUEUE_ERROR_QUEUE_ABORTED");
   } else {
-    j->status = bgv_verify(j->c->ctx, &j->b, j->job_result, NULL, &j->stats);
+    switch (j->kind) {
+      case K_PARTIAL:
+        j->status = bgv_partial(j->c->ctx, &j->b, j->miller, NULL, j->job_result, &j->ok);
+        j->c->partial_jobs = j->b.n_jobs;
+        if (j->status == BGV_OK) {
+          j->status = bgv_last_stats(j->c->ctx, &j->stats);
+          j->stats.pubkeys_aggregated = j->b.n_sets ? j->pk_off[j->b.n_sets] : 0;
+        }
+        break;
+      case K_FINISH:
+        j->b.n_jobs = j->c->partial_jobs;
+        j->job_result = (int32_t*)calloc(j->b.n_jobs ? j->b.n_jobs : 1, 4);
+        j->status = j->job_result ? bgv_partial_finish(j->c->ctx, j->job_result, &j->stats) : BGV_E_INVALID_ARG;
+        break;
+      case K_COMBINE: j->status = bgv_combine_final(j->c->ctx, j->parts, j->n_parts, &j->ok); break;
+      default: j->status = bgv_verify(j->c->ctx, &j->b, j->job_result, NULL, &j->stats); break;
+    }
     if (j->status != BGV_OK) snprintf(j->err, sizeof j->err, "bgv error %d: %s", j->status, bgv_last_error());
   }
   j->t_end_ms = now_ms();
@@ -347,6 +384,16 @@ static napi_value result_object(napi_env env, const verify_job* j) {
   napi_set_named_property(env, o, "workerStartMs", v);
   napi_create_double(env, j->t_end_ms, &v);
   napi_set_named_property(env, o, "workerEndMs", v);
+  if (j->kind == K_PARTIAL) {
+    void* dst = NULL;
+    napi_value ab;
+    if (napi_create_arraybuffer(env, 576, &dst, &ab) != napi_ok) return NULL;
+    memcpy(dst, j->miller, 576);
+    napi_create_typedarray(env, napi_uint8_array, 576, ab, 0, &v);
+    napi_set_named_property(env, o, "miller", v);
+    napi_get_boolean(env, j->ok != 0, &v);
+    napi_set_named_property(env, o, "ok", v);
+  }
   return o;
 }
 
@@ -366,6 +413,10 @@ static void done_verify(napi_env env, napi_status st, void* data) { /* main thre
     napi_create_string_utf8(env, j->err, NAPI_AUTO_LENGTH, &msg);
     napi_create_error(env, NULL, msg, &err);
     napi_reject_deferred(env, j->deferred, err);
+  } else if (j->kind == K_COMBINE) {
+    napi_value b;
+    napi_get_boolean(env, j->ok != 0, &b);
+    napi_resolve_deferred(env, j->deferred, b);
   } else {
     napi_resolve_deferred(env, j->deferred, result_object(env, j));
   }
@@ -377,7 +428,18 @@ static void done_verify(napi_env env, napi_status st, void* data) { /* main thre
   free(j);
 }
 
-static napi_value Verify(napi_env env, napi_callback_info info) {
+/* queue j on the libuv pool; the promise settles in done_verify */
+static napi_value queue_job(napi_env env, napi_value ctx_val, verify_job* j, const char* label) {
+  napi_create_reference(env, ctx_val, 1, &j->ctx_ref); /* the context outlives its queued work */
+  napi_value promise, name;
+  NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
+  NAPI_CALL(env, napi_create_string_utf8(env, label, NAPI_AUTO_LENGTH, &name));
+  NAPI_CALL(env, napi_create_async_work(env, NULL, name, exec_verify, done_verify, j, &j->work));
+  NAPI_CALL(env, napi_queue_async_work(env, j->work));
+  return promise;
+}
+
+static napi_value queue_batch(napi_env env, napi_callback_info info, int kind, const char* label) {
   size_t argc = 2;
   napi_value a[2];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, a, NULL, NULL));
@@ -385,6 +447,7 @@ static napi_value Verify(napi_env env, napi_callback_info info) {
   if (!c) return NULL;
   verify_job* j = (verify_job*)calloc(1, sizeof *j);
   j->c = c;
+  j->kind = kind;
   if (read_batch(env, a[1], j, 1)) {
     for (int k = 0; k < N_FIELDS; k++)
       if (j->refs[k]) napi_delete_reference(env, j->refs[k]);
@@ -392,14 +455,46 @@ static napi_value Verify(napi_env env, napi_callback_info info) {
     free(j);
     return NULL;
   }
-  napi_create_reference(env, a[0], 1, &j->ctx_ref); /* the context outlives its queued work */
   j->job_result = (int32_t*)calloc(j->b.n_jobs ? j->b.n_jobs : 1, 4);
-  napi_value promise, name;
-  NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
-  NAPI_CALL(env, napi_create_string_utf8(env, "bgv_verify", NAPI_AUTO_LENGTH, &name));
-  NAPI_CALL(env, napi_create_async_work(env, NULL, name, exec_verify, done_verify, j, &j->work));
-  NAPI_CALL(env, napi_queue_async_work(env, j->work));
-  return promise;
+  return queue_job(env, a[0], j, label);
+}
+
+static napi_value Verify(napi_env env, napi_callback_info info) { return queue_batch(env, info, K_VERIFY, "bgv_verify"); }
+
+static napi_value Partial(napi_env env, napi_callback_info info) { return queue_batch(env, info, K_PARTIAL, "bgv_partial"); }
+
+/* partialFinish(ctx): the shard left by the last partial() on the context */
+static napi_value PartialFinish(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value a[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, a, NULL, NULL));
+  addon_ctx* c = get_ctx(env, a[0]);
+  if (!c) return NULL;
+  verify_job* j = (verify_job*)calloc(1, sizeof *j);
+  j->c = c;
+  j->kind = K_FINISH; /* results sized on the pool thread from the pending partial */
+  return queue_job(env, a[0], j, "bgv_partial_finish");
+}
+
+static napi_value CombineFinal(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value a[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, a, NULL, NULL));
+  addon_ctx* c = get_ctx(env, a[0]);
+  if (!c) return NULL;
+  void* data;
+  size_t len;
+  if (argc < 2 || typed(env, a[1], napi_uint8_array, &data, &len) || len % 576) {
+    napi_throw_type_error(env, NULL, "combineFinal(ctx, Uint8Array of 576-byte partials)");
+    return NULL;
+  }
+  verify_job* j = (verify_job*)calloc(1, sizeof *j);
+  j->c = c;
+  j->kind = K_COMBINE;
+  j->n_parts = (uint32_t)(len / 576);
+  j->parts = (uint8_t*)malloc(len ? len : 1); /* copied: the caller may reuse its buffer */
+  if (len) memcpy(j->parts, data, len);
+  return queue_job(env, a[0], j, "bgv_combine_final");
 }
 
 static napi_value VerifySync(napi_env env, napi_callback_info info) {
@@ -435,6 +530,9 @@ static napi_value Init(napi_env env, napi_value exports) {
       {"pubkeysValidate", NULL, PubkeysValidate, NULL, NULL, NULL, napi_enumerable, NULL},
       {"verify", NULL, Verify, NULL, NULL, NULL, napi_enumerable, NULL},
       {"verifySync", NULL, VerifySync, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"partial", NULL, Partial, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"partialFinish", NULL, PartialFinish, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"combineFinal", NULL, CombineFinal, NULL, NULL, NULL, napi_enumerable, NULL},
   };
   if (napi_define_properties(env, exports, sizeof d / sizeof d[0], d) != napi_ok) return NULL;
   return exports;

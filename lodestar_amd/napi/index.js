@@ -25,6 +25,12 @@
 // the HBM index2pubkey table) or {raw: Uint8Array(96)} (uncompressed x||y).
 const path = require("path");
 
+// Every context's device batch runs on a libuv pool thread; contexts on
+// different devices run concurrently only if the pool has a thread for each
+// (default 4).  The pool is created on first use, so this must run before any
+// async work of the process (INTEGRATION.md section 4).
+if (!process.env.UV_THREADPOOL_SIZE) process.env.UV_THREADPOOL_SIZE = "16";
+
 const addon = require(path.join(__dirname, "bgv.node"));
 
 const MAX_SIGNATURE_SETS_PER_JOB = 128; // multithread/index.ts:39
@@ -32,6 +38,15 @@ const MAX_BUFFERED_SIGS = 32; // multithread/index.ts:48
 const MAX_BUFFER_WAIT_MS = 100; // multithread/index.ts:57
 const MAX_JOBS_CAN_ACCEPT_WORK = 512; // multithread/index.ts:62
 const MAX_SETS_PER_DEVICE_BATCH = 1 << 17;
+// a device batch of at least this many sets (and >= 2 jobs) is split by job
+// over the idle devices (partial Miller products, ONE combined final
+// exponentiation); smaller batches run whole on one device while the other
+// devices take the next batch (lodestar_amd/verifier.py SHARD_MIN_SETS)
+const SHARD_MIN_SETS = 4096;
+// non-batchable jobs start once a macro task passes without a new job
+// (bounded), so the per-block calls of a range-sync segment
+// (verifyBlocksSignatures.ts:30-47, sleep(0) every 8 blocks) coalesce
+const MAX_QUIET_WAITS = 8;
 const RAW_BIT = 0x80000000;
 const EMPTY_JOB = -10; // BGV internal code: a job without sets
 
@@ -108,6 +123,21 @@ function encodeJobs(jobs) {
   return {jobOffsets, pkOffsets, pkIndices: Uint32Array.from(idx.length ? idx : [0]), msgs, sigs, sigLen, rawPks};
 }
 
+// whole jobs to `world` shards, greedy by set count (largest first), job
+// order kept inside a shard (lodestar_amd/dist.py shard_jobs)
+function shardJobs(sizes, world) {
+  const shards = Array.from({length: world}, () => []);
+  const load = new Array(world).fill(0);
+  const order = sizes.map((s, j) => j).sort((a, b) => sizes[b] - sizes[a] || a - b);
+  for (const j of order) {
+    let r = 0;
+    for (let k = 1; k < world; k++) if (load[k] < load[r]) r = k;
+    shards[r].push(j);
+    load[r] += Math.max(sizes[j], 1);
+  }
+  return shards.map((s) => s.sort((a, b) => a - b));
+}
+
 function jobOutcome(r) {
   if (r === 1) return {ok: true, value: true};
   if (r === 0) return {ok: true, value: false};
@@ -142,26 +172,42 @@ function observe(h, v) {
 }
 
 class BlsGpuVerifier {
-  constructor({device = 0, maxSetsPerDeviceBatch = MAX_SETS_PER_DEVICE_BATCH} = {}) {
-    this.ctx = addon.open(device);
+  // devices: HIP device ordinals, one context each, all owned by this process
+  // (chain/chain.ts:199-202 constructs one verifier per node); every context
+  // holds a replica of the pubkey table
+  constructor({device = 0, devices = null, maxSetsPerDeviceBatch = MAX_SETS_PER_DEVICE_BATCH, shardMinSets = SHARD_MIN_SETS} = {}) {
+    const ids = devices && devices.length ? devices : [device];
+    this.ctxs = ids.map((d) => addon.open(d));
+    this.ctx = this.ctxs[0];
+    this.idle = ids.map(() => true);
     this.maxSetsPerDeviceBatch = maxSetsPerDeviceBatch;
+    this.shardMinSets = shardMinSets;
     this.jobs = [];
+    this.queuedSets = 0;
     this.bufferedJobs = null;
-    this.busy = 0; // device batches in flight (one context = one worker)
+    this.busy = 0; // device batches in flight
     this.closed = false;
+    this.runScheduled = false;
+    this.pushSeq = 0;
+    this.seenSeq = 0;
+    this.quietWaits = 0;
     this.metrics = newMetrics();
     this.runJob = this.runJob.bind(this);
     this.runBufferedJobs = this.runBufferedJobs.bind(this);
   }
 
-  // syncPubkeys / addPubkey (pubkeyCache.ts:56-77): 48-byte compressed keys
+  // syncPubkeys / addPubkey (pubkeyCache.ts:56-77): 48-byte compressed keys, every replica
   syncPubkeys(firstIndex, pubkeys48) {
-    addon.pubkeysSet(this.ctx, firstIndex, pubkeys48, 0);
+    for (const c of this.ctxs) addon.pubkeysSet(c, firstIndex, pubkeys48, 0);
   }
 
-  // multithread/index.ts:143-149 with the context as the only worker
+  // multithread/index.ts:143-149.  A queued job joins the next device batch,
+  // so work is accepted while fewer than MAX_JOBS_CAN_ACCEPT_WORK jobs and
+  // less than one full device batch of sets are queued, batch in flight or
+  // not (gating on idle devices would stop the network processor,
+  // network/processor/index.ts:406, for every 5-40 ms device batch)
   canAcceptWork() {
-    return !this.closed && this.busy < 1 && this.jobs.length < MAX_JOBS_CAN_ACCEPT_WORK;
+    return !this.closed && this.jobs.length < MAX_JOBS_CAN_ACCEPT_WORK && this.queuedSets < this.maxSetsPerDeviceBatch;
   }
 
   async verifySignatureSets(sets, opts = {}) {
@@ -169,8 +215,10 @@ class BlsGpuVerifier {
     checkSets(sets);
     this.metrics.lodestar_bls_aggregated_pubkeys_total += aggregatedPubkeysCount(sets);
     if (opts.verifyOnMainThread) {
-      // high priority, unbuffered: one synchronous device batch
-      const res = addon.verifySync(this.ctx, encodeJobs([sets]));
+      // high priority, unbuffered: one synchronous device batch (an idle
+      // context if there is one; the context mutex serialises otherwise)
+      const k = Math.max(0, this.idle.indexOf(true));
+      const res = addon.verifySync(this.ctxs[k], encodeJobs([sets]));
       this.recordWork([{sets}], res);
       const o = jobOutcome(res.results[0]);
       if (!o.ok) throw o.error;
@@ -199,18 +247,31 @@ class BlsGpuVerifier {
           this.runBufferedJobs();
         }
       } else {
-        this.jobs.push(job);
-        setTimeout(this.runJob, 0);
+        this.pushJobs([job]);
+        this.pushSeq++;
+        this.scheduleRun();
       }
     });
   }
 
-  // multithread/index.ts:425-431
+  pushJobs(jobs) {
+    for (const j of jobs) this.queuedSets += j.sets.length;
+    this.jobs.push(...jobs);
+  }
+
+  scheduleRun() {
+    if (!this.runScheduled) {
+      this.runScheduled = true;
+      setTimeout(this.runJob, 0);
+    }
+  }
+
+  // multithread/index.ts:425-431 (the buffer has already waited: no quiet window)
   runBufferedJobs() {
     if (this.bufferedJobs) {
-      this.jobs.push(...this.bufferedJobs.jobs);
+      this.pushJobs(this.bufferedJobs.jobs);
       this.bufferedJobs = null;
-      setTimeout(this.runJob, 0);
+      this.scheduleRun();
     }
   }
 
@@ -223,14 +284,37 @@ class BlsGpuVerifier {
       jobs.push(job);
       totalSigs += job.sets.length;
     }
+    this.queuedSets -= totalSigs;
     return jobs;
   }
 
-  // multithread/index.ts:297-391
-  async runJob() {
-    if (this.closed || this.busy >= 1) return;
-    const jobs = this.prepareWork();
-    if (jobs.length === 0) return;
+  // multithread/index.ts:297-391: every idle device takes a device batch; a
+  // batch of >= shardMinSets sets is split over all idle devices instead
+  runJob() {
+    this.runScheduled = false;
+    while (!this.closed && this.jobs.length > 0) {
+      const idle = [];
+      this.idle.forEach((f, k) => f && idle.push(k));
+      if (idle.length === 0) return; // a finishing batch reschedules
+      if (this.pushSeq !== this.seenSeq && this.quietWaits < MAX_QUIET_WAITS) {
+        // jobs arrived since the last look: wait one more macro task
+        this.seenSeq = this.pushSeq;
+        this.quietWaits++;
+        this.scheduleRun();
+        return;
+      }
+      this.quietWaits = 0;
+      this.seenSeq = this.pushSeq;
+      const jobs = this.prepareWork();
+      let n = 0;
+      for (const j of jobs) n += j.sets.length;
+      const devs = idle.length > 1 && jobs.length > 1 && n >= this.shardMinSets ? idle : [idle[0]];
+      for (const k of devs) this.idle[k] = false;
+      this.runDeviceBatch(jobs, devs);
+    }
+  }
+
+  async runDeviceBatch(jobs, devs) {
     this.busy++;
     const m = this.metrics;
     try {
@@ -243,7 +327,9 @@ class BlsGpuVerifier {
       m.lodestar_bls_thread_pool_job_groups_started_total += 1;
       m.lodestar_bls_thread_pool_jobs_started_total += jobs.length;
       m.lodestar_bls_thread_pool_sig_sets_started_total += started;
-      const res = await addon.verify(this.ctx, encodeJobs(jobs.map((j) => j.sets)));
+      const res = devs.length === 1
+        ? await addon.verify(this.ctxs[devs[0]], encodeJobs(jobs.map((j) => j.sets)))
+        : await this.verifySharded(jobs.map((j) => j.sets), devs);
       this.recordWork(jobs, res);
       jobs.forEach((job, k) => {
         const o = jobOutcome(res.results[k]);
@@ -254,7 +340,44 @@ class BlsGpuVerifier {
       for (const job of jobs) job.reject(e);
     }
     this.busy--;
-    setTimeout(this.runJob, 0);
+    for (const k of devs) this.idle[k] = true;
+    this.scheduleRun();
+  }
+
+  // SURVEY 8e: jobs sharded by set count over the devices, one partial Miller
+  // product per shard (bgv_partial, concurrently on the libuv pool), ONE final
+  // exponentiation of their product (bgv_combine_final); only when it fails
+  // does each shard localise its failing jobs (bgv_partial_finish, the
+  // worker's per-job retry).  Returns the result shape of addon.verify.
+  async verifySharded(jobSets, devs) {
+    const shards = shardJobs(jobSets.map((s) => s.length), devs.length);
+    const live = [];
+    shards.forEach((ids, r) => ids.length && live.push({ctx: this.ctxs[devs[r]], ids}));
+    if (live.length === 1) return addon.verify(live[0].ctx, encodeJobs(jobSets));
+    const parts = await Promise.all(live.map((s) => addon.partial(s.ctx, encodeJobs(s.ids.map((k) => jobSets[k])))));
+    const millers = new Uint8Array(576 * live.length);
+    parts.forEach((p, k) => millers.set(p.miller, 576 * k));
+    const valid = await addon.combineFinal(live[0].ctx, millers);
+    // a verifyOnMainThread call that ran on a context in between replaced its
+    // pending partial (bgv error -7): that shard is verified again from scratch
+    const finals = valid ? parts : await Promise.all(live.map((s) => addon.partialFinish(s.ctx).catch((e) => {
+      if (!/bgv error -7/.test(e.message)) throw e;
+      return addon.verify(s.ctx, encodeJobs(s.ids.map((k) => jobSets[k])));
+    })));
+    const results = new Int32Array(jobSets.length);
+    let sigsOk = 0;
+    live.forEach((s, k) => s.ids.forEach((j, i) => {
+      results[j] = finals[k].results[i];
+      if (valid && results[j] === 1) sigsOk += jobSets[j].length;
+    }));
+    return {
+      results, batchRetries: valid ? 0 : 1, batchSigsSuccess: sigsOk,
+      pubkeysAggregated: parts.reduce((a, p) => a + p.pubkeysAggregated, 0),
+      deviceMs: Math.max(...parts.map((p) => p.deviceMs)),
+      workerStartMs: Math.min(...parts.map((p) => p.workerStartMs)),
+      workerEndMs: Math.max(...finals.map((p) => p.workerEndMs)),
+      shards: live.length,
+    };
   }
 
   recordWork(jobs, res) {
@@ -277,7 +400,7 @@ class BlsGpuVerifier {
   // gauges sampled at scrape time (index.ts:135-139)
   metricsSnapshot() {
     this.metrics.lodestar_bls_thread_pool_queue_length = this.jobs.length;
-    this.metrics.lodestar_bls_thread_pool_workers_busy = this.busy;
+    this.metrics.lodestar_bls_thread_pool_workers_busy = this.idle.filter((f) => !f).length;
     return this.metrics;
   }
 
@@ -292,11 +415,12 @@ class BlsGpuVerifier {
     }
     for (const job of this.jobs) job.reject(new QueueError());
     this.jobs = [];
-    addon.close(this.ctx); // waits for the batch in flight (the context mutex)
+    this.queuedSets = 0;
+    for (const c of this.ctxs) addon.close(c); // each waits for its batch in flight (the context mutex)
   }
 }
 
 module.exports = {
-  addon, BlsGpuVerifier, QueueError, chunkifyMaximizeChunkSize, encodeJobs, checkSets,
-  MAX_BUFFERED_SIGS, MAX_BUFFER_WAIT_MS, MAX_JOBS_CAN_ACCEPT_WORK,
+  addon, BlsGpuVerifier, QueueError, chunkifyMaximizeChunkSize, encodeJobs, checkSets, shardJobs,
+  MAX_BUFFERED_SIGS, MAX_BUFFER_WAIT_MS, MAX_JOBS_CAN_ACCEPT_WORK, SHARD_MIN_SETS,
 };

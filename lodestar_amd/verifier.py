@@ -44,12 +44,20 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import native
+from .dist import shard_jobs
 
 MAX_SIGNATURE_SETS_PER_JOB = 128  # multithread/index.ts:39
 MAX_BUFFERED_SIGS = 32            # multithread/index.ts:48
 MAX_BUFFER_WAIT_MS = 100          # multithread/index.ts:57
 MAX_JOBS_CAN_ACCEPT_WORK = 512    # multithread/index.ts:62
 MAX_SETS_PER_DEVICE_BATCH = 1 << 17
+# a device batch of at least this many sets (and >= 2 jobs) is split by job
+# over the idle devices: each returns a partial Miller product and ONE final
+# exponentiation checks their product.  Below it the batch runs
+# whole on one device and other devices take the next batch: one GPU verifies
+# 2,000-4,000 sets in 7-10 ms, within ~2 ms of the split, which pays a host
+# round trip and the combined final exponentiation
+SHARD_MIN_SETS = 4096
 
 
 class BlsError(Exception):
@@ -275,14 +283,22 @@ class _Job:
 
 
 class BlsGpuVerifier:
-    """``IBlsVerifier`` on one or more MI355X devices.
+    """``IBlsVerifier`` on one or more MI355X devices, one context per device
+    (one host process owns them all, as the reference's pool owns its workers,
+    chain/chain.ts:199-202).
 
-    devices: HIP device ordinals.  Jobs of one device batch are split by job
-    across devices (each device holds a replica of the pubkey table)."""
+    devices: HIP device ordinals; every device holds a replica of the pubkey
+    table.  Every idle device takes a device batch of the queued jobs; a batch
+    of >= ``shard_min_sets`` sets is split by job over all idle devices instead,
+    each returning a partial Miller product (bgv_partial), combined by ONE
+    final exponentiation (bgv_combine_final); when that check fails every
+    shard localises its own failing jobs (bgv_partial_finish)."""
 
     def __init__(self, devices=(0,), metrics: dict | None = None, scalar_seed: int | None = None,
-                 max_sets_per_device_batch: int = MAX_SETS_PER_DEVICE_BATCH):
+                 max_sets_per_device_batch: int = MAX_SETS_PER_DEVICE_BATCH, shard_min_sets: int = SHARD_MIN_SETS):
         self.devices = [native.Device(d) for d in devices]
+        self._shard_min = shard_min_sets
+        self._idle = [True] * len(self.devices)
         self.table = PubkeyTable(self.devices)
         self.metrics = metrics if metrics is not None else _new_metrics()
         self._rng = np.random.default_rng(scalar_seed) if scalar_seed is not None else None
@@ -293,13 +309,19 @@ class BlsGpuVerifier:
         self._buffer_handle = None
         self._closed = False
         self._busy = 0
-        self._exec = ThreadPoolExecutor(max_workers=len(self.devices))
+        self._exec = ThreadPoolExecutor(max_workers=len(self.devices) + 1)  # + the main-thread path
         self._dev_locks = [threading.Lock() for _ in self.devices]
 
     # -- IBlsVerifier ---------------------------------------------------
     def can_accept_work(self) -> bool:
-        """multithread/index.ts:143-149 (device count stands in for workers)"""
-        return self._busy < len(self.devices) and len(self._jobs) < MAX_JOBS_CAN_ACCEPT_WORK
+        """multithread/index.ts:143-149.  A queued job joins the next device
+        batch, so work is accepted while the queue holds fewer than
+        MAX_JOBS_CAN_ACCEPT_WORK jobs and less than one full device batch of
+        sets, whether or not a batch is in flight (a GPU wants large batches;
+        gating on idle devices would stall the network processor for every
+        batch, network/processor/index.ts:406)."""
+        return (not self._closed and len(self._jobs) < MAX_JOBS_CAN_ACCEPT_WORK
+                and sum(len(j.sets) for j in self._jobs) < self._max_batch)
 
     async def verify_signature_sets(self, sets: list[ISignatureSet], opts: VerifySignatureOpts | None = None) -> bool:
         opts = opts or VerifySignatureOpts()
@@ -310,7 +332,7 @@ class BlsGpuVerifier:
         check_sets(sets)
         if opts.verifyOnMainThread:
             # unbuffered, high priority: one device batch right now
-            res = await asyncio.get_running_loop().run_in_executor(self._exec, self._run_device_batch, [sets])
+            res = await asyncio.get_running_loop().run_in_executor(self._exec, self._run_device_batch, [sets], [0])
             r = res[0]
             if isinstance(r, Exception):
                 raise r
@@ -340,7 +362,7 @@ class BlsGpuVerifier:
         """maybeBatch.ts:16-38 for one job, synchronously (BlsSingleThreadVerifier
         path, singleThread.ts:14-35)."""
         check_sets(sets)
-        r = self._run_device_batch([sets])[0]
+        r = self._run_device_batch([sets], [0])[0]
         if isinstance(r, Exception):
             raise r
         return r
@@ -394,23 +416,28 @@ class BlsGpuVerifier:
         asyncio.get_running_loop().call_soon(self._schedule)
 
     def _schedule(self):
-        if self._closed or not self._jobs or self._busy >= 1:
-            return
-        take, n = [], 0
-        while self._jobs and (n == 0 or n + len(self._jobs[0].sets) <= self._max_batch):
-            j = self._jobs.pop(0)
-            take.append(j)
-            n += len(j.sets)
-        self._busy += 1
-        asyncio.ensure_future(self._run(take))
+        """every idle device takes a device batch of the queued jobs; a large
+        batch is split over all idle devices (SHARD_MIN_SETS)"""
+        while not self._closed and self._jobs and any(self._idle):
+            take, n = [], 0
+            while self._jobs and (n == 0 or n + len(self._jobs[0].sets) <= self._max_batch):
+                j = self._jobs.pop(0)
+                take.append(j)
+                n += len(j.sets)
+            idle = [d for d, f in enumerate(self._idle) if f]
+            devs = idle if (len(idle) > 1 and len(take) > 1 and n >= self._shard_min) else idle[:1]
+            for d in devs:
+                self._idle[d] = False
+            self._busy += 1
+            asyncio.ensure_future(self._run(take, devs))
 
-    async def _run(self, jobs: list[_Job]):
+    async def _run(self, jobs: list[_Job], devs: list[int]):
         loop = asyncio.get_running_loop()
         try:
             now = time.monotonic()
             for j in jobs:
                 self.metrics["job_wait_time_s"].append(now - j.added)
-            results = await loop.run_in_executor(self._exec, self._run_device_batch, [j.sets for j in jobs])
+            results = await loop.run_in_executor(self._exec, self._run_device_batch, [j.sets for j in jobs], devs)
             for j, r in zip(jobs, results):
                 if j.future.done():
                     continue
@@ -424,6 +451,8 @@ class BlsGpuVerifier:
                     j.future.set_exception(e)
         finally:
             self._busy -= 1
+            for d in devs:
+                self._idle[d] = True
             loop.call_soon(self._schedule)
 
     # -- device -------------------------------------------------------------
@@ -433,52 +462,110 @@ class BlsGpuVerifier:
         s = self._rng.integers(1, 2**64 - 1, size=max(n, 1), dtype=np.uint64, endpoint=True)
         return s
 
-    def _run_device_batch(self, jobs: list[list[ISignatureSet]]) -> list:
-        """Verify a list of jobs; returns per job True / False / BlsError."""
+    @staticmethod
+    def _verdict(r: int):
+        return True if r == 1 else False if r == 0 else error_for_code(-r)
+
+    def _record(self, st: native.BgvStats, seconds: float):
+        self.metrics["batch_retries"] += int(st.batch_retries)
+        self.metrics["batch_sigs_success"] += int(st.batch_sigs_success)
+        self.metrics["device_time_s"] += seconds
+
+    def _run_device_batch(self, jobs: list[list[ISignatureSet]], devs: list[int] | None = None) -> list:
+        """Verify a list of jobs on the devices `devs` (default: all); returns
+        per job True / False / BlsError.  One device: bgv_verify.  Several: the
+        jobs are sharded by set count (dist.shard_jobs), every shard reduced to
+        a partial Miller product, the partials combined by one final
+        exponentiation, and only when that fails each shard localised on its
+        own device."""
         if not jobs:
             return []
-        # shard whole jobs across devices, balanced by set count (SURVEY §8e)
-        nd = len(self.devices)
-        shards: list[list[int]] = [[] for _ in range(nd)]
-        load = [0] * nd
-        for k in sorted(range(len(jobs)), key=lambda k: -len(jobs[k])):
-            d = load.index(min(load))
-            shards[d].append(k)
-            load[d] += max(len(jobs[k]), 1)
+        devs = list(range(len(self.devices))) if devs is None else list(devs)
+        shards = shard_jobs([len(j) for j in jobs], len(devs)) if len(devs) > 1 else [list(range(len(jobs)))]
+        live = [(devs[r], ids) for r, ids in enumerate(shards) if ids]
         out: list = [None] * len(jobs)
-
-        def run_shard(d: int):
-            ids = sorted(shards[d])
-            if not ids:
-                return
-            sub = [jobs[k] for k in ids]
+        self.metrics["sets_started"] += sum(len(j) for j in jobs)
+        self.metrics["jobs_started"] += len(jobs)
+        if len(live) == 1:
+            d, ids = live[0]
             try:
-                arrays = encode_jobs(sub, self._scalars(sum(len(j) for j in sub)))
+                arrays = encode_jobs(jobs, self._scalars(sum(len(j) for j in jobs)))
                 with self._dev_locks[d]:
                     t0 = time.perf_counter()
                     jr, _ = self.devices[d].verify(arrays, want_set_codes=False)
-                    st = self.devices[d].last_stats
-                    self.metrics["batch_retries"] += int(st.batch_retries)
-                    self.metrics["batch_sigs_success"] += int(st.batch_sigs_success)
-                    self.metrics["device_time_s"] += time.perf_counter() - t0
-            except Exception as e:  # noqa: BLE001 -- a device error rejects this shard's jobs (index.ts:386-393)
-                for k in ids:
-                    out[k] = e
-                return
-            for k, r in zip(ids, jr.tolist()):
-                out[k] = True if r == 1 else False if r == 0 else error_for_code(-r)
+                    self._record(self.devices[d].last_stats, time.perf_counter() - t0)
+            except Exception as e:  # noqa: BLE001 -- a device error rejects the package (index.ts:386-393)
+                return [e] * len(jobs)
+            return [self._verdict(r) for r in jr.tolist()]
+        # every participating context stays locked from its partial to its
+        # localisation (the partial's intermediates live on the context)
+        locks = [self._dev_locks[d] for d, _ in sorted(live)]
+        for lk in locks:
+            lk.acquire()
+        try:
+            t0 = time.perf_counter()
+            parts: list = [None] * len(live)
 
-        if nd == 1:
-            run_shard(0)
-        else:
-            ths = [threading.Thread(target=run_shard, args=(d,)) for d in range(nd)]
-            for t in ths:
-                t.start()
-            for t in ths:
-                t.join()
-        self.metrics["sets_started"] += sum(len(j) for j in jobs)
-        self.metrics["jobs_started"] += len(jobs)
+            def run_partial(k):
+                d, ids = live[k]
+                try:
+                    sub = [jobs[i] for i in ids]
+                    parts[k] = self.devices[d].partial(encode_jobs(sub, self._scalars(sum(len(j) for j in sub))))
+                except Exception as e:  # noqa: BLE001
+                    parts[k] = e
+
+            self._parallel(run_partial, len(live))
+            failed = [k for k in range(len(live)) if isinstance(parts[k], Exception)]
+            for k in failed:  # a device error rejects that shard's jobs
+                for i in live[k][1]:
+                    out[i] = parts[k]
+            ok_shards = [k for k in range(len(live)) if k not in failed]
+            if not ok_shards:
+                return out
+            d0 = live[ok_shards[0]][0]
+            valid = self.devices[d0].combine_final([parts[k][0] for k in ok_shards])
+            finals: list = [None] * len(live)
+            if valid:
+                for k in ok_shards:
+                    finals[k] = parts[k][2]  # provisional: 1, or -code for a rejected job (final)
+            else:
+                def run_finish(k):
+                    try:
+                        finals[k] = self.devices[live[k][0]].partial_finish()
+                    except Exception as e:  # noqa: BLE001
+                        finals[k] = e
+
+                self._parallel(run_finish, len(live), only=ok_shards)
+            valid_sets = 0
+            for k in ok_shards:
+                ids = live[k][1]
+                if isinstance(finals[k], Exception):
+                    for i in ids:
+                        out[i] = finals[k]
+                    continue
+                for i, r in zip(ids, np.asarray(finals[k]).tolist()):
+                    out[i] = self._verdict(int(r))
+                    if valid and r == 1:
+                        valid_sets += len(jobs[i])
+            self.metrics["batch_retries"] += 0 if valid else 1
+            self.metrics["batch_sigs_success"] += valid_sets
+            self.metrics["device_time_s"] += time.perf_counter() - t0
+        finally:
+            for lk in locks:
+                lk.release()
         return out
+
+    @staticmethod
+    def _parallel(fn, n: int, only=None):
+        ks = list(range(n)) if only is None else list(only)
+        if len(ks) == 1:
+            fn(ks[0])
+            return
+        ths = [threading.Thread(target=fn, args=(k,)) for k in ks]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
 
 
 async def reject_first_invalid_resolve_all_valid(is_valid_awaitables) -> dict:
@@ -519,7 +606,7 @@ async def verify_blocks_signatures(bls: "BlsGpuVerifier", blocks_sets: list[list
         for chunk in chunkify_maximize_chunk_size(sets, MAX_SIGNATURE_SETS_PER_JOB):
             jobs.append(chunk)
             owner.append(b)
-    res = await asyncio.get_running_loop().run_in_executor(bls._exec, bls._run_device_batch, jobs)
+    res = await asyncio.get_running_loop().run_in_executor(bls._exec, bls._run_device_batch, jobs, None)
     ok = [True] * len(blocks_sets)
     for b, r in zip(owner, res):
         if isinstance(r, Exception):

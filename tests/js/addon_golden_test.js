@@ -45,6 +45,15 @@ function goldenBatch(v) {
   };
 }
 
+// the golden jobs as arrays of IBlsVerifier sets (raw pubkeys or table indices)
+function goldenJobSets(v) {
+  return v.jobs.map((j) => j.sets.map((s) => {
+    const sig = hex(s.sig);
+    const pks = s.raw !== null ? [{raw: hex(v.raw_pubkeys[s.raw])}] : s.pk.map((i) => ({index: i}));
+    return {type: "aggregate", pubkeys: pks, signingRoot: hex(s.msg), signature: sig};
+  }));
+}
+
 async function main() {
   const v = JSON.parse(fs.readFileSync(path.join(golden, "batch_vectors.json")));
   const interop = JSON.parse(fs.readFileSync(path.join(golden, "interop-pubkeys.json")));
@@ -131,7 +140,63 @@ async function main() {
   assert.strictEqual(m.lodestar_bls_aggregated_pubkeys_total, 5 + 1);  // the k=5 aggregate (+ the empty one)
   assert.strictEqual(verifier.metricsSnapshot().lodestar_bls_thread_pool_queue_length, 0);
 
-  // 4. close(): buffered and queued jobs reject with QueueError QUEUE_ABORTED
+  // 4. range-sync call pattern (verifyBlocksSignatures.ts:30-47): one
+  // non-batchable call per block, sleep(0) after every 8 blocks; the quiet
+  // window coalesces the segment's blocks into at most two device batches
+  const sleep0 = () => new Promise((r) => setTimeout(r, 0));
+  groups = m.lodestar_bls_thread_pool_job_groups_started_total;
+  const blockPromises = [];
+  for (let i = 0; i < 32; i++) {
+    blockPromises.push(verifier.verifySignatureSets(i === 19 ? wrongMsg : sets));
+    if ((i + 1) % 8 === 0) await sleep0();
+  }
+  const blockRes = await Promise.all(blockPromises);
+  const cs2Batches = m.lodestar_bls_thread_pool_job_groups_started_total - groups;
+  assert.deepStrictEqual(blockRes.map((r, i) => r === (i !== 19)), new Array(32).fill(true));
+  assert.ok(cs2Batches <= 2, `32 per-block calls took ${cs2Batches} device batches`);
+  console.log(`range-sync pattern: 32 per-block calls -> ${cs2Batches} device batch(es)`);
+
+  // 5. back-pressure: queued work joins the next batch, so canAcceptWork stays
+  // true while a batch is in flight and turns false once a full next batch
+  // (maxSetsPerDeviceBatch sets) is queued
+  const small = new BlsGpuVerifier({device: 0, maxSetsPerDeviceBatch: 2 * sets.length});
+  small.syncPubkeys(0, pk48);
+  const inflight = small.verifySignatureSets(sets);
+  await sleep0();
+  await sleep0();
+  assert.strictEqual(small.canAcceptWork(), true, "accepts while a batch is in flight");
+  const q1 = small.verifySignatureSets(sets);
+  const q2 = small.verifySignatureSets(sets);
+  assert.strictEqual(small.canAcceptWork(), false, "a full next batch is queued");
+  assert.deepStrictEqual(await Promise.all([inflight, q1, q2]), [true, true, true]);
+  assert.strictEqual(small.canAcceptWork(), true);
+  await small.close();
+
+  // 6. several devices owned by one process (SURVEY 8e): two contexts (both on
+  // GPU 0 here) verify one batch split by job; partial Miller products, ONE
+  // combined final exponentiation; a failing shard is localised per job
+  const multi = new BlsGpuVerifier({devices: [0, 0], shardMinSets: 1});
+  multi.syncPubkeys(0, pk48);
+  multi.ctxs.forEach((c) => addon.pubkeysSet(c, v.extra_table_base, extra, 1));
+  const jobSets = v.jobs.map((j) => j.sets);
+  const mres = await multi.verifySharded(goldenJobSets(v), [0, 1]);
+  assert.strictEqual(mres.shards, 2);
+  assert.deepStrictEqual(Array.from(mres.results), expected, "sharded golden batch (faulted shards) vs golden");
+  assert.deepStrictEqual(Array.from(mres.results), Array.from(got.results), "sharded == bgv_verify");
+  assert.strictEqual(mres.batchRetries, 1);
+  const clean = v.jobs.map((j, k) => k).filter((k) => v.jobs[k].expected === 1);
+  const cres = await multi.verifySharded(clean.map((k) => goldenJobSets(v)[k]), [0, 1]);
+  assert.deepStrictEqual(Array.from(cres.results), clean.map(() => 1), "sharded clean batch");
+  assert.strictEqual(cres.batchRetries, 0);
+  // and through the pool: 32 block-sized calls split over both contexts
+  const before = multi.metrics.lodestar_bls_thread_pool_job_groups_started_total;
+  const segRes = await Promise.all(Array.from({length: 8}, (_, i) => multi.verifySignatureSets(i === 5 ? wrongMsg : sets)));
+  assert.deepStrictEqual(segRes, segRes.map((_, i) => i !== 5));
+  assert.ok(multi.metrics.lodestar_bls_thread_pool_job_groups_started_total - before >= 1);
+  void jobSets;
+  await multi.close();
+
+  // 7. close(): buffered and queued jobs reject with QueueError QUEUE_ABORTED
   const pending = verifier.verifySignatureSets(sets, {batchable: true});
   await verifier.close();
   await assert.rejects(pending, (e) => e instanceof QueueError && e.type.code === "QUEUE_ERROR_QUEUE_ABORTED");

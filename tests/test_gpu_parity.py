@@ -427,3 +427,54 @@ def test_two_level_job_fold_bit_identical():
         finally:
             d.close()
     assert outs["0"] == outs["1"]
+
+
+def test_multi_device_verifier_partial_combine():
+    """BlsGpuVerifier over two contexts (both on GPU 0 here: the code path of
+    one process owning several GPUs): a device batch split by job,
+    one partial Miller product per context (bgv_partial), ONE combined final
+    exponentiation (bgv_combine_final) and, when it fails, per-shard
+    localisation (bgv_partial_finish).  Verdicts equal a one-context
+    bgv_verify of the same jobs, clean and with faulted shards; the golden
+    jobs (rejections of every kind) give their golden verdicts."""
+    from lodestar_amd import native
+    from lodestar_amd import verifier as V
+    pool = V.BlsGpuVerifier(devices=(0, 0), shard_min_sets=1)
+    single = native.Device(0)
+    try:
+        for d in pool.devices + [single]:
+            G.load_golden_table(d)
+            first = d.pubkeys_count()
+            d.gen_keys(first, 256, 5)
+        syn, bad = _synthetic_on(single, 240, 8, first, 256, 11, fault_every=29)
+        syn["n_jobs"] = 12
+        syn["job_offsets"] = (np.arange(13) * 20).astype(np.uint32)
+        jobs = G.sets_from_arrays(syn)
+        want = [not bad[k * 20:(k + 1) * 20].any() for k in range(12)]
+        jr1, _ = single.verify(syn)
+        assert jr1.tolist() == [int(w) for w in want]
+        retries = pool.metrics["batch_retries"]
+        got = pool._run_device_batch(jobs)  # split over both contexts
+        assert got == want
+        assert pool.metrics["batch_retries"] == retries + 1
+        clean = [j for j, w in zip(jobs, want) if w]
+        assert pool._run_device_batch(clean) == [True] * len(clean)
+        assert pool.metrics["batch_retries"] == retries + 1
+        # golden jobs: rejected jobs stay rejected with their codes
+        ga, gexp, _ = G.golden_arrays(scalars_seed=9)
+        raw = ga["raw_pks"].reshape(-1, 96)
+        gjobs = [[V.ISignatureSet(V.SignatureSetType.aggregate, s.signingRoot, s.signature,
+                                  pubkeys=[V.PublicKey(raw=raw[p.index & 0x7FFFFFFF].tobytes()) if p.index & 0x80000000 else p
+                                           for p in ([s.pubkey] if s.pubkey else s.pubkeys)])
+                  for s in job] for job in G.sets_from_arrays(dict(ga, sigs=ga["sigs"].reshape(-1, 192),
+                                                                   msgs=ga["msgs"].reshape(-1, 32)))]
+        res = pool._run_device_batch(gjobs)
+        assert [1 if r is True else 0 if r is False else -r.code for r in res] == gexp
+
+        async def run():  # through the queue: block-sized calls split over both contexts
+            return await asyncio.gather(*[pool.verify_signature_sets(j) for j in jobs])
+
+        assert asyncio.run(run()) == want
+    finally:
+        single.close()
+        asyncio.run(pool.close())
