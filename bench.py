@@ -124,8 +124,10 @@ def pmc_traffic(stage: str):
 
 
 def cpu_baseline(budget_s: float = 12.0):
-    """oracle C restatement (oracle/libbls_ref.so) timed on ALL of this host's
-    usable cores on a bounded sample of the same workload; None when not built."""
+    """oracle C restatement (oracle/libbls_ref.so: mulx/adx Montgomery, multi-pair
+    Miller loop with a shared squaring) timed on the threads this host's cgroup
+    grants, on bounded samples of every config with the reference pool's
+    semantics (oracle/cref.py bench_configs); None when not built."""
     try:
         from oracle import cref
     except Exception as e:  # noqa: BLE001
@@ -134,7 +136,9 @@ def cpu_baseline(budget_s: float = 12.0):
     affinity = len(os.sched_getaffinity(0))
     quota = cgroup_cpu_quota()
     threads = min(affinity, quota) if quota else affinity
-    out = cref.bench_segment_sample(budget_s=budget_s, seed=SEED, threads=threads)
+    per = cref.bench_configs(threads=threads, budget_s=budget_s, seed=SEED)
+    out = dict(per["c4"])  # the metric's config (C4) at the top level
+    out["per_config"] = {k: v for k, v in per.items() if k != "c4"}
     phys = physical_cores()
     out["cores_affinity"] = affinity
     out["cgroup_cpu_quota"] = quota

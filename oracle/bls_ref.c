@@ -22,6 +22,7 @@
  *   hash_to_G2: RFC 9380 BLS12381G2_XMD:SHA-256_SSWU_RO_ with the POP DST
  */
 #include <stdint.h>
+#include <x86intrin.h>
 #include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
@@ -70,37 +71,35 @@ static void sub_p(uint64_t* a) {
     br = (uint64_t)(d >> 64) & 1;
   }
 }
-static void fp_add(fp* r, const fp* a, const fp* b) {
-  uint64_t c = 0;
-  for (int i = 0; i < 6; i++) {
-    u128 s = (u128)a->l[i] + b->l[i] + c;
-    r->l[i] = (uint64_t)s;
-    c = (uint64_t)(s >> 64);
-  }
-  if (geq_p(r->l)) sub_p(r->l);
+/* modular add / sub on adc / sbb chains, branch-free selection */
+static inline void fp_add(fp* r, const fp* a, const fp* b) {
+  unsigned long long t[6], u[6];
+  unsigned char c = 0, br = 0;
+  for (int i = 0; i < 6; i++) c = _addcarry_u64(c, a->l[i], b->l[i], &t[i]);
+  for (int i = 0; i < 6; i++) br = _subborrow_u64(br, t[i], PM[i], &u[i]);
+  const uint64_t keep = -(uint64_t)br; /* t < p: keep t (a + b < 2p < 2^384: no carry out) */
+  for (int i = 0; i < 6; i++) r->l[i] = (t[i] & keep) | (u[i] & ~keep);
 }
-static void fp_sub(fp* r, const fp* a, const fp* b) {
-  uint64_t br = 0;
-  for (int i = 0; i < 6; i++) {
-    u128 d = (u128)a->l[i] - b->l[i] - br;
-    r->l[i] = (uint64_t)d;
-    br = (uint64_t)(d >> 64) & 1;
-  }
-  if (br) {
-    uint64_t c = 0;
-    for (int i = 0; i < 6; i++) {
-      u128 s = (u128)r->l[i] + PM[i] + c;
-      r->l[i] = (uint64_t)s;
-      c = (uint64_t)(s >> 64);
-    }
-  }
+static inline void fp_sub(fp* r, const fp* a, const fp* b) {
+  unsigned long long t[6];
+  unsigned char br = 0, c = 0;
+  for (int i = 0; i < 6; i++) br = _subborrow_u64(br, a->l[i], b->l[i], &t[i]);
+  const uint64_t m = -(uint64_t)br;
+  for (int i = 0; i < 6; i++) c = _addcarry_u64(c, t[i], PM[i] & m, (unsigned long long*)&r->l[i]);
 }
-static void fp_neg(fp* r, const fp* a) {
-  fp z;
-  memset(&z, 0, sizeof z);
+static inline void fp_neg(fp* r, const fp* a) {
+  static const fp z;
   fp_sub(r, &z, a);
 }
-static void fp_mul(fp* r, const fp* a, const fp* b) {
+#include "bls_ref_mulx.h"
+static uint64_t PMX[7]; /* p, then -p^-1 mod 2^64 (fp_mul_mulx) */
+static int use_mulx = 0; /* the CPU has BMI2 + ADX (bref_init) */
+static void fp_mul_portable(fp* r, const fp* a, const fp* b);
+static inline void fp_mul(fp* r, const fp* a, const fp* b) {
+  if (use_mulx) fp_mul_mulx(r->l, a->l, b->l, PMX);
+  else fp_mul_portable(r, a, b);
+}
+static void fp_mul_portable(fp* r, const fp* a, const fp* b) {
   uint64_t t[8] = {0};
   for (int i = 0; i < 6; i++) {
     uint64_t c = 0;
@@ -128,16 +127,75 @@ static void fp_mul(fp* r, const fp* a, const fp* b) {
   memcpy(r->l, t, 48);
 }
 static void fp_sqr(fp* r, const fp* a) { fp_mul(r, a, a); }
+/* a^e, 4-bit fixed window (e plain, 6 limbs) */
 static void fp_pow(fp* r, const fp* a, const fp* e) {
-  fp acc = FONE;
-  for (int i = 5; i >= 0; i--)
-    for (int b = 63; b >= 0; b--) {
-      fp_sqr(&acc, &acc);
-      if ((e->l[i] >> b) & 1) fp_mul(&acc, &acc, a);
+  fp tab[16], acc = FONE;
+  tab[0] = FONE;
+  tab[1] = *a;
+  for (int i = 2; i < 16; i++) fp_mul(&tab[i], &tab[i - 1], a);
+  int started = 0;
+  for (int w = 95; w >= 0; w--) {
+    const unsigned d = (unsigned)(e->l[w >> 4] >> (4 * (w & 15))) & 15u;
+    if (started) {
+      fp_sqr(&acc, &acc); fp_sqr(&acc, &acc); fp_sqr(&acc, &acc); fp_sqr(&acc, &acc);
+      if (d) fp_mul(&acc, &acc, &tab[d]);
+    } else if (d) {
+      acc = tab[d];
+      started = 1;
     }
+  }
   *r = acc;
 }
-static void fp_inv(fp* r, const fp* a) { fp_pow(r, a, &E_PM2); }
+/* plain 6-limb helpers for the binary inversion */
+static inline int u384_is_one(const uint64_t* a) { return a[0] == 1 && !(a[1] | a[2] | a[3] | a[4] | a[5]); }
+static inline int u384_geq(const uint64_t* a, const uint64_t* b) {
+  for (int i = 5; i >= 0; i--) if (a[i] != b[i]) return a[i] > b[i];
+  return 1;
+}
+static inline void u384_sub(uint64_t* a, const uint64_t* b) {
+  unsigned char br = 0;
+  for (int i = 0; i < 6; i++) br = _subborrow_u64(br, a[i], b[i], (unsigned long long*)&a[i]);
+}
+static inline void u384_shr1(uint64_t* a) {
+  for (int i = 0; i < 5; i++) a[i] = (a[i] >> 1) | (a[i + 1] << 63);
+  a[5] >>= 1;
+}
+/* x / 2 mod p for x < p (plain) */
+static inline void half_mod_p(uint64_t* x) {
+  if (x[0] & 1) {
+    unsigned char c = 0;
+    unsigned long long t[6];
+    for (int i = 0; i < 6; i++) c = _addcarry_u64(c, x[i], PM[i], &t[i]);
+    for (int i = 0; i < 5; i++) x[i] = (t[i] >> 1) | (t[i + 1] << 63);
+    x[5] = (t[5] >> 1) | ((uint64_t)c << 63);
+  } else {
+    u384_shr1(x);
+  }
+}
+static fp R3; /* R^3 mod p, Montgomery form of R^2 */
+/* Montgomery inverse by the binary extended Euclid on the plain value A = aR:
+ * x = A^-1 mod p, then x R^3 R^-1 = R^2 / A = a^-1 R.  Not constant time: the
+ * oracle and the CPU baseline verify public data. */
+static void fp_inv(fp* r, const fp* a) {
+  uint64_t u[6], v[6], x1[6] = {1, 0, 0, 0, 0, 0}, x2[6] = {0};
+  memcpy(u, a->l, 48);
+  memcpy(v, PM, 48);
+  if (!(u[0] | u[1] | u[2] | u[3] | u[4] | u[5])) { memset(r, 0, sizeof *r); return; }
+  while (!u384_is_one(u) && !u384_is_one(v)) {
+    while (!(u[0] & 1)) { u384_shr1(u); half_mod_p(x1); }
+    while (!(v[0] & 1)) { u384_shr1(v); half_mod_p(x2); }
+    if (u384_geq(u, v)) {
+      u384_sub(u, v);
+      fp_sub((fp*)x1, (const fp*)x1, (const fp*)x2);
+    } else {
+      u384_sub(v, u);
+      fp_sub((fp*)x2, (const fp*)x2, (const fp*)x1);
+    }
+  }
+  fp x;
+  memcpy(x.l, u384_is_one(u) ? x1 : x2, 48);
+  fp_mul(r, &x, &R3);
+}
 static int fp_sqrt(fp* r, const fp* a) {
   fp s, c;
   fp_pow(&s, a, &E_SQRT);
@@ -242,53 +300,39 @@ static void f2_inv(fp2* r, const fp2* a) {
   fp_mul(&t, &a->c1, &n);
   fp_neg(&r->c1, &t);
 }
-static void f2_pow(fp2* r, const fp2* a, const fp* e) {
-  fp2 acc;
-  acc.c0 = FONE;
-  memset(&acc.c1, 0, sizeof(fp));
-  for (int i = 5; i >= 0; i--)
-    for (int b = 63; b >= 0; b--) {
-      f2_sqr(&acc, &acc);
-      if ((e->l[i] >> b) & 1) f2_mul(&acc, &acc, a);
-    }
-  *r = acc;
+/* Fp2 square root by two Fp exponentiations (p = 3 mod 4), the norm method
+ * of the device (lodestar_amd/csrc/fp2.h fp2_sqrt): d = sqrt(a0^2 + a1^2)
+ * exists iff a is a square; t = (a0 + d)/2, s = t^((p-3)/4); s^2 t == 1 gives
+ * x = s t + (a1 s / 2) i, otherwise x = (a1 s / 2) - (s t) i.  Any root is
+ * fine: callers fix the sign (sgn0 / lexicographic flag). */
+static void f2_sqrt_tail(fp2* r, const fp2* a, const fp* d) {
+  fp t, s, st, s2t, as;
+  fp_add(&t, &a->c0, d);
+  fp_mul(&t, &t, &FHALF);
+  fp_pow(&s, &t, &E_P34);
+  fp_mul(&st, &s, &t);
+  fp_mul(&s2t, &st, &s);
+  fp_mul(&as, &a->c1, &s);
+  fp_mul(&as, &as, &FHALF);
+  if (fp_eq(&s2t, &FONE)) { r->c0 = st; r->c1 = as; }
+  else { r->c0 = as; fp_neg(&r->c1, &st); }
 }
-static int f2_is_square(const fp2* a) {
-  fp n, l;
-  f2_norm(&n, a);
-  if (fp_is_zero(&n)) return 1;
-  fp_pow(&l, &n, &E_LEG);
-  return fp_eq(&l, &FONE);
-}
-/* Fp2 square root, q = p = 3 mod 4 (Adj & Rodriguez-Henriquez, Alg. 9) */
 static int f2_sqrt(fp2* r, const fp2* a) {
-  fp2 a1, alpha, a0, x0, t, minus1;
-  minus1.c0 = FONE;
-  fp_neg(&minus1.c0, &minus1.c0);
-  memset(&minus1.c1, 0, sizeof(fp));
-  f2_pow(&a1, a, &E_P34);
-  f2_mul(&t, &a1, a);
-  f2_mul(&alpha, &a1, &t);
-  fp2 ac;
-  f2_conj(&ac, &alpha); /* alpha^p */
-  f2_mul(&a0, &ac, &alpha);
-  if (f2_eq(&a0, &minus1)) return 0;
-  x0 = t; /* a1 * a */
-  if (f2_eq(&alpha, &minus1)) {
-    /* x = i * x0 */
-    fp2 ix;
-    fp_neg(&ix.c0, &x0.c1);
-    ix.c1 = x0.c0;
-    *r = ix;
-  } else {
-    fp2 one1 = alpha, b;
-    fp_add(&one1.c0, &one1.c0, &FONE);
-    f2_pow(&b, &one1, &E_LEG);
-    f2_mul(r, &b, &x0);
+  if (fp_is_zero(&a->c1)) {
+    fp s;
+    if (fp_sqrt(&s, &a->c0)) { r->c0 = s; memset(&r->c1, 0, sizeof(fp)); return 1; }
+    fp na;
+    fp_neg(&na, &a->c0); /* -1 is a non-residue: -a0 is a square, x = sqrt(-a0) i */
+    fp_sqrt(&s, &na);
+    memset(&r->c0, 0, sizeof(fp));
+    r->c1 = s;
+    return 1;
   }
-  fp2 chk;
-  f2_sqr(&chk, r);
-  return f2_eq(&chk, a);
+  fp n, d;
+  f2_norm(&n, a);
+  if (!fp_sqrt(&d, &n)) return 0;
+  f2_sqrt_tail(r, a, &d);
+  return 1;
 }
 static int f2_sgn0(const fp2* a) {
   int s0 = fp_parity(&a->c0), z0 = fp_is_zero(&a->c0), s1 = fp_parity(&a->c1);
@@ -374,15 +418,37 @@ static void f12_inv(fp12* r, const fp12* a) {
   f6_mul(&t1, &a->c1, &t0);
   f6_neg(&r->c1, &t1);
 }
-/* multiply by the sparse line a0 + a1 w^2 + b1 w^3 (schoolbook on the
- * non-zero slots: c0 = (a0, a1, 0), c1 = (0, b1, 0)) */
+/* multiply by the sparse line l = a0 + a1 w^2 + b1 w^3, i.e. l0 = (a0, a1, 0)
+ * and l1 = (0, b1, 0) in Fp12 = Fp6[w]: Karatsuba over w with sparse Fp6
+ * products, 13 Fp2 multiplications instead of 18 */
+static void f6_mul_01(fp6* r, const fp6* a, const fp2* b0, const fp2* b1) { /* a * (b0 + b1 v) */
+  fp2 t0, t1, u, s0, s1, c0, c1, c2;
+  f2_mul(&t0, &a->c0, b0);
+  f2_mul(&t1, &a->c1, b1);
+  f2_add(&s0, &a->c1, &a->c2); f2_mul(&u, &s0, b1); f2_sub(&u, &u, &t1); f2_mul_xi(&u, &u); f2_add(&c0, &u, &t0);
+  f2_add(&s0, &a->c0, &a->c1); f2_add(&s1, b0, b1); f2_mul(&u, &s0, &s1); f2_sub(&u, &u, &t0); f2_sub(&c1, &u, &t1);
+  f2_add(&s0, &a->c0, &a->c2); f2_mul(&u, &s0, b0); f2_sub(&u, &u, &t0); f2_add(&c2, &u, &t1);
+  r->c0 = c0; r->c1 = c1; r->c2 = c2;
+}
+static void f6_mul_1(fp6* r, const fp6* a, const fp2* b1) { /* a * (b1 v) */
+  fp2 c0, c1, c2;
+  f2_mul(&c0, &a->c2, b1); f2_mul_xi(&c0, &c0);
+  f2_mul(&c1, &a->c0, b1);
+  f2_mul(&c2, &a->c1, b1);
+  r->c0 = c0; r->c1 = c1; r->c2 = c2;
+}
 static void f12_mul_line(fp12* f, const fp2* a0, const fp2* a1, const fp2* b1) {
-  fp12 l;
-  memset(&l, 0, sizeof l);
-  l.c0.c0 = *a0;
-  l.c0.c1 = *a1;
-  l.c1.c1 = *b1;
-  f12_mul(f, f, &l);
+  fp6 t0, t1, s;
+  fp2 ab;
+  f6_mul_01(&t0, &f->c0, a0, a1);
+  f6_mul_1(&t1, &f->c1, b1);
+  f6_add(&s, &f->c0, &f->c1);
+  f2_add(&ab, a1, b1);
+  f6_mul_01(&s, &s, a0, &ab);
+  f6_sub(&s, &s, &t0);
+  f6_sub(&f->c1, &s, &t1);
+  f6_mul_v(&t1, &t1);
+  f6_add(&f->c0, &t0, &t1);
 }
 static void f12_frob(fp12* r, const fp12* a, int k) {
   fp2 c[6] = {a->c0.c0, a->c1.c0, a->c0.c1, a->c1.c1, a->c0.c2, a->c1.c2};
@@ -433,7 +499,7 @@ static void final_exp(fp12* r, const fp12* f) {
 }
 
 /* ---------------------------------------------------------- curves */
-#define JAC_IMPL(G, F, ADD, SUB, MUL, SQR, DBLF, ISZ, EQ, ONE_SET)                         \
+#define JAC_IMPL(G, F, ADD, SUB, MUL, SQR, DBLF, ISZ, EQ, ONE_SET, ONE_Z)                         \
   static void G##_dbl(G* r, const G* p) {                                                  \
     F A, B, C, D, E, FF, t, x3, y3, z3;                                                    \
     SQR(&A, &p->x); SQR(&B, &p->y); SQR(&C, &B);                                           \
@@ -461,6 +527,23 @@ static void final_exp(fp12* r, const fp12* f) {
     ADD(&z3, &p->z, &q->z); SQR(&z3, &z3); SUB(&z3, &z3, &z1z1); SUB(&z3, &z3, &z2z2);     \
     MUL(&z3, &z3, &h);                                                                     \
     r->x = x3; r->y = y3; r->z = z3;                                                       \
+  }                                                                                        \
+  /* p + (qx, qy, 1) (madd-2007-bl); same exceptional cases */                             \
+  static void G##_add_aff(G* r, const G* p, const F* qx, const F* qy) {                    \
+    if (ISZ(&p->z)) { r->x = *qx; r->y = *qy; ONE_Z(&r->z); return; }                      \
+    F z1z1, u2, s2, h, hh, i, j, rr, v, t, x3, y3, z3;                                     \
+    SQR(&z1z1, &p->z); MUL(&u2, qx, &z1z1); MUL(&s2, qy, &p->z); MUL(&s2, &s2, &z1z1);     \
+    SUB(&h, &u2, &p->x); SUB(&rr, &s2, &p->y);                                             \
+    if (ISZ(&h)) {                                                                         \
+      if (ISZ(&rr)) { G##_dbl(r, p); return; }                                             \
+      ONE_SET(r); return;                                                                  \
+    }                                                                                      \
+    SQR(&hh, &h); DBLF(&i, &hh); DBLF(&i, &i); MUL(&j, &h, &i); DBLF(&rr, &rr);             \
+    MUL(&v, &p->x, &i);                                                                    \
+    SQR(&x3, &rr); SUB(&x3, &x3, &j); SUB(&x3, &x3, &v); SUB(&x3, &x3, &v);                \
+    SUB(&t, &v, &x3); MUL(&y3, &rr, &t); MUL(&t, &p->y, &j); DBLF(&t, &t); SUB(&y3, &y3, &t); \
+    ADD(&z3, &p->z, &h); SQR(&z3, &z3); SUB(&z3, &z3, &z1z1); SUB(&z3, &z3, &hh);          \
+    r->x = x3; r->y = y3; r->z = z3;                                                       \
   }
 
 static void fp_dbl(fp* r, const fp* a) { fp_add(r, a, a); }
@@ -470,8 +553,10 @@ static void g2_set_inf(g2j* r) {
   r->x.c0 = FONE;
   r->y.c0 = FONE;
 }
-JAC_IMPL(g1j, fp, fp_add, fp_sub, fp_mul, fp_sqr, fp_dbl, fp_is_zero, fp_eq, g1_set_inf)
-JAC_IMPL(g2j, fp2, f2_add, f2_sub, f2_mul, f2_sqr, f2_dbl, f2_is_zero, f2_eq, g2_set_inf)
+static void fp_one_z(fp* z) { *z = FONE; }
+static void f2_one_z(fp2* z) { memset(z, 0, sizeof *z); z->c0 = FONE; }
+JAC_IMPL(g1j, fp, fp_add, fp_sub, fp_mul, fp_sqr, fp_dbl, fp_is_zero, fp_eq, g1_set_inf, fp_one_z)
+JAC_IMPL(g2j, fp2, f2_add, f2_sub, f2_mul, f2_sqr, f2_dbl, f2_is_zero, f2_eq, g2_set_inf, f2_one_z)
 
 static void g1_from_aff(g1j* r, const g1a* a) { r->x = a->x; r->y = a->y; r->z = FONE; }
 static void g2_from_aff(g2j* r, const g2a* a) {
@@ -491,21 +576,32 @@ static void g2_to_aff(g2a* r, const g2j* p) {
   f2_inv(&zi, &p->z); f2_sqr(&z2, &zi); f2_mul(&z3, &z2, &zi);
   f2_mul(&r->x, &p->x, &z2); f2_mul(&r->y, &p->y, &z3); r->inf = 0;
 }
+/* [k]P by double-and-add; mixed additions when P has Z = 1 */
 static void g1_mul_u64(g1j* r, const g1j* p, uint64_t k) {
   g1j acc;
   g1_set_inf(&acc);
+  const int aff = fp_eq(&p->z, &FONE);
   for (int b = 63; b >= 0; b--) {
     g1j_dbl(&acc, &acc);
-    if ((k >> b) & 1) g1j_add(&acc, &acc, p);
+    if ((k >> b) & 1) {
+      if (aff) g1j_add_aff(&acc, &acc, &p->x, &p->y);
+      else g1j_add(&acc, &acc, p);
+    }
   }
   *r = acc;
 }
 static void g2_mul_u64(g2j* r, const g2j* p, uint64_t k) {
   g2j acc;
   g2_set_inf(&acc);
+  fp2 one;
+  f2_one_z(&one);
+  const int aff = f2_eq(&p->z, &one);
   for (int b = 63; b >= 0; b--) {
     g2j_dbl(&acc, &acc);
-    if ((k >> b) & 1) g2j_add(&acc, &acc, p);
+    if ((k >> b) & 1) {
+      if (aff) g2j_add_aff(&acc, &acc, &p->x, &p->y);
+      else g2j_add(&acc, &acc, p);
+    }
   }
   *r = acc;
 }
@@ -737,6 +833,11 @@ static void fp_from_64be(fp* r, const uint8_t* b) { /* 64 bytes big-endian mod p
   fp_mul(&t, &hi, &T256);
   fp_add(r, &t, &lo);
 }
+/* simplified SWU onto E2' (RFC 9380 6.6.2) with the device's shortcut
+ * (lodestar_amd/csrc/h2c.h map_to_curve_sswu): one exponentiation of
+ * norm(gx1) answers the square test and starts the root; when gx1 is not a
+ * square, sqrt(norm(gx2)) = sqrt(-norm(Z)^3) norm(u)^3 d. */
+static fp SQRT_NEG_NZ3;
 static void map_sswu(g2a* out, const fp2* u) {
   fp2 u2, zu2, den, tv, x1, x2, gx1, gx2, t, x, g, y;
   f2_sqr(&u2, u);
@@ -752,8 +853,21 @@ static void map_sswu(g2a* out, const fp2* u) {
   f2_sqr(&t, &x1); f2_add(&t, &t, &S_A); f2_mul(&gx1, &t, &x1); f2_add(&gx1, &gx1, &S_B);
   f2_mul(&x2, &zu2, &x1);
   f2_sqr(&t, &x2); f2_add(&t, &t, &S_A); f2_mul(&gx2, &t, &x2); f2_add(&gx2, &gx2, &S_B);
-  if (f2_is_square(&gx1)) { x = x1; g = gx1; } else { x = x2; g = gx2; }
-  f2_sqrt(&y, &g);
+  fp n1, d, chk, nu, nu3;
+  f2_norm(&n1, &gx1);
+  fp_pow(&d, &n1, &E_SQRT);
+  fp_sqr(&chk, &d);
+  const int sq = fp_eq(&chk, &n1);
+  if (sq) { x = x1; g = gx1; }
+  else {
+    x = x2; g = gx2;
+    f2_norm(&nu, u);
+    fp_sqr(&nu3, &nu); fp_mul(&nu3, &nu3, &nu);
+    fp_mul(&d, &d, &nu3);
+    fp_mul(&d, &d, &SQRT_NEG_NZ3);
+  }
+  if (fp_is_zero(&g.c1) || (!sq && f2_is_zero(&den))) f2_sqrt(&y, &g);
+  else f2_sqrt_tail(&y, &g, &d);
   if (f2_sgn0(u) != f2_sgn0(&y)) f2_neg(&y, &y);
   out->x = x; out->y = y; out->inf = 0;
 }
@@ -864,6 +978,10 @@ static void exp_consts(void) {
 }
 void bref_init(void) {
   if (inited) return;
+  memcpy(PMX, PM, 48);
+  PMX[6] = PINV;
+  __builtin_cpu_init();
+  use_mulx = __builtin_cpu_supports("bmi2") && __builtin_cpu_supports("adx");
   /* R mod p and R^2 mod p by doubling (plain arithmetic mod p via fp_add) */
   fp one;
   memset(&one, 0, sizeof one);
@@ -874,6 +992,9 @@ void bref_init(void) {
   for (int i = 0; i < 384; i++) fp_add(&x, &x, &x);
   R2 = x;
   FONE = R1;
+  memcpy(PMX, PM, 48);
+  PMX[6] = PINV;
+  fp_mul(&R3, &R2, &R2);
   exp_consts();
   fp two = FONE;
   fp_add(&two, &two, &two);
@@ -903,6 +1024,12 @@ void bref_init(void) {
   f2_inv(&ia, &S_A);
   f2_mul(&t, &S_B, &ia); f2_neg(&S_MBA, &t);
   f2_mul(&t, &S_Z, &S_A); f2_inv(&t, &t); f2_mul(&S_BZA, &S_B, &t);
+  {
+    fp nz, nz3;
+    f2_norm(&nz, &S_Z);
+    fp_sqr(&nz3, &nz); fp_mul(&nz3, &nz3, &nz); fp_neg(&nz3, &nz3);
+    fp_sqrt(&SQRT_NEG_NZ3, &nz3); /* -norm(Z)^3 is a square */
+  }
   T256 = FONE;
   for (int i = 0; i < 256; i++) fp_add(&T256, &T256, &T256); /* 2^256, Montgomery */
   inited = 1;
@@ -972,9 +1099,7 @@ void bref_aggregate(const uint8_t* pks96, int k, uint8_t* out96) {
     g1a a;
     g1_decode96(&a, pks96 + 96 * i);
     if (a.inf) continue;
-    g1j j;
-    g1_from_aff(&j, &a);
-    g1j_add(&acc, &acc, &j);
+    g1j_add_aff(&acc, &acc, &a.x, &a.y);
   }
   g1_serialize(out96, &acc);
 }
@@ -1058,9 +1183,7 @@ static void* bench_worker(void* arg) {
       for (uint32_t k = c->pk_off[beg + i]; k < c->pk_off[beg + i + 1]; k++) {
         g1a a;
         g1_decode96(&a, c->table96 + 96ull * c->pk_idx[k]);
-        g1j pj;
-        g1_from_aff(&pj, &a);
-        g1j_add(&acc, &acc, &pj);
+        if (!a.inf) g1j_add_aff(&acc, &acc, &a.x, &a.y);
       }
       g1_to_aff(&K[i], &acc);
       if (!code) code = sig_from_bytes(&S[i], c->sigs + 192ull * (beg + i), (int)c->sig_len[beg + i]);

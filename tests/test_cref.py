@@ -77,3 +77,11 @@ def test_aggregate_matches_python(C):
     p = B.sk_to_pk(9)
     assert C.aggregate([B.g1_serialize(p)] * 2) == B.g1_serialize(B.E1.add(p, p))
     assert C.aggregate([B.g1_serialize(p), B.g1_serialize(B.E1.neg(p))]) == B.g1_serialize(None)
+
+
+def test_mulx_header_is_generated():
+    """oracle/bls_ref_mulx.h is the output of tools/gen_cref_mulx.py"""
+    import os
+    from tools import gen_cref_mulx
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    assert open(os.path.join(root, "oracle", "bls_ref_mulx.h")).read() == gen_cref_mulx.gen()
