@@ -177,6 +177,7 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
     if (k.miller != -1 && k.miller != 1 && !lanes_ok(k.miller)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.miller %d", k.miller);
     if (k.job_lanes != 0 && !lanes_ok(k.job_lanes)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.job_lanes %d", k.job_lanes);
     if (k.pairs < 0 || k.pairs > 2) return fail(BGV_E_INVALID_ARG, "bgv_cfg.pairs %d", k.pairs);
+    if (k.msm < -1 || k.msm > 2) return fail(BGV_E_INVALID_ARG, "bgv_cfg.msm %d", k.msm);
     if (k.defer_pct < -1 || k.defer_pct > 100) return fail(BGV_E_INVALID_ARG, "bgv_cfg.defer_pct %d", k.defer_pct);
   }
   int n = 0;
@@ -472,18 +473,25 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   //  * latency mode (two-lane hash maps, cooperative G2) below SPLIT_MAX
   //    (25,088 sets: 24.5 ms split against 26.3 ms; 50,176: 35.4 against 29.3);
   //  * two pairs per Miller work item only when the batch alone fills the chip.
-  static const uint32_t MILLER_COOP_MAX = 6000, SPLIT_MAX = 35000, PAIRS2_MIN = 65536;
+  static const uint32_t MILLER18_MIN = 2000, MILLER6_MIN = 6000, MILLER1_MIN = 35000, MSM_MIN = 6000, SPLIT_MAX = 35000,
+                        PAIRS2_MIN = 65536;
   const bgv_cfg& k = c->cfg;
   d.pairs_per_item = k.pairs ? (uint32_t)k.pairs : (n >= PAIRS2_MIN ? 2u : 1u);
   d.split = k.split >= 0 ? (uint32_t)k.split : (n < SPLIT_MAX ? 1u : 0u);
-  // Deferred subgroup checks (bulk mode): the signature stage decodes, and the
-  // checks of sets [defer_from, n) run beside the Miller loops
-  // (bgv_kernels.hip k_job_recode).  All of them with one pair per Miller item
-  // (C4/2 28.3 -> 26.4 ms); half with two pairs per item: the Miller kernel
-  // leaves 240 SIMDs to the MSM tail and the job pairs, and half of the checks
-  // fill them without outlasting it (C4, 3 runs each: none 39.75, 50% 39.27,
-  // 65% 39.31, all 39.89 ms).  defer_from is a multiple of 64 (wave-uniform).
-  const int pct = d.split ? 0 : (k.defer_pct >= 0 ? k.defer_pct : (d.pairs_per_item == 2 ? 50 : 100));
+  // sum r_i sigma_i per job by a bucket MSM (16 x 4-bit windows, one
+  // workgroup per job, k_msm_fused) when jobs are block-sized (<= 256 sets)
+  d.msm = k.msm >= 0 ? (uint32_t)k.msm : ((n >= MSM_MIN && d.span_log2 <= 8) ? 1u : 0u);
+  // Deferred subgroup checks: the signature stage only decodes, and the checks
+  // of sets [defer_from, n) run beside the Miller loops (bgv_kernels.hip
+  // k_job_recode).  Wherever the MSM sums the signatures (the latency mode
+  // without it checks beside the per-set scaling, k_sig_split_coop): all of
+  // them with one pair per Miller item (C4/2 28.3 -> 26.4 ms); half with two
+  // pairs per item: the Miller kernel leaves 240 SIMDs to the MSM tail and
+  // the job pairs, and half of the checks fill them without outlasting it
+  // (C4, 3 runs each: none 39.75, 50% 39.27, 65% 39.31, all 39.89 ms).
+  // defer_from is a multiple of 64 (wave-uniform).
+  const bool deferrable = !d.split || d.msm;
+  const int pct = !deferrable ? 0 : (k.defer_pct >= 0 ? k.defer_pct : (!d.split && d.pairs_per_item == 2 ? 50 : 100));
   d.defer_grp = pct > 0 ? 1u : 0u;
   d.defer_from = pct > 0 ? (uint32_t)(((uint64_t)n * (uint32_t)(100 - pct) / 100u) & ~63ull) : n;
   // two-level per-job fold (bgv_tail.hip) when few jobs of >= 64 sets leave
@@ -494,16 +502,16 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
     const bool on = k.prefold >= 0 ? (k.prefold && d.span_log2 >= 2 && d.span_log2 <= 8) : few_big;
     d.prefold_log2 = on ? (d.span_log2 + 1) / 2 : 0u;
   }
-  d.miller_coop = k.miller >= 0 ? (k.miller == 1 ? 0u : (uint32_t)k.miller) : (n < MILLER_COOP_MAX ? 36u : 0u);
+  // set-pair Miller layout: lanes per pair shrink as the batch grows, so the
+  // waves stay near one per SIMD (a pair's loop is a chain of ~1,800 Fp2
+  // products on 6 lanes, ~560 product rounds on 36)
+  d.miller_coop = k.miller >= 0 ? (k.miller == 1 ? 0u : (uint32_t)k.miller)
+                                : (n < MILLER18_MIN ? 36u : n < MILLER6_MIN ? 18u : n < MILLER1_MIN ? 6u : 0u);
   // fixed-argument lines (pairing.h miller_lines): the G2 half of the one-lane
   // Miller loop moves to the hash stream, phase 1 (C4 40.4 -> 39.5 ms); with
   // one pair per item it loses (C4/2 26.4 -> 28.5 ms)
   d.lines = (uint32_t)(!d.split && !d.miller_coop && (k.lines >= 0 ? k.lines : d.pairs_per_item == 2));
   d.job_lanes = k.job_lanes ? (uint32_t)k.job_lanes : 36u;
-  // sum r_i sigma_i per job by a bucket MSM (16 x 4-bit windows, ~1,800 G2
-  // additions per 98-set job instead of 98 x 75 in per-set scalar mults)
-  // when jobs are block-sized (<= 256 sets)
-  d.msm = k.msm >= 0 ? (uint32_t)k.msm : ((n >= MILLER_COOP_MAX && d.span_log2 <= 8) ? 1u : 0u);
   if (b->scalars && !b->on_device) {
     // staged with the other host arrays above
   } else if (b->scalars) {
@@ -556,7 +564,7 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
     w.lines = c->lines.p;
   }
   w.msm_bucket = nullptr; w.msm_mask = nullptr; w.msm_win = nullptr;
-  if (d.msm) {
+  if (d.msm == 2) {
     if ((r = c->msm_bucket.ensure(nj * 16 * 15)) || (r = c->msm_mask.ensure(nj * 16)) || (r = c->msm_win.ensure(nj * 16))) return r;
     w.msm_bucket = c->msm_bucket.p; w.msm_mask = c->msm_mask.p; w.msm_win = c->msm_win.p;
   }

@@ -583,6 +583,133 @@ __global__ void BGV_BULK k_msm_job(dev_batch b, dev_work w) {
   w.job_code[j] = code;
 }
 
+// ------------------------------------------ fused per-job MSM (msm mode)
+// One 256-lane workgroup per job computes S_job = sum_i r_i sigma_i with no
+// bucket in HBM: lane (w, d) = (tid >> 4, tid & 15) owns bucket d of window
+// w (4-bit windows of the 64-bit scalars).
+//   1. counting sort, in LDS, of the job's sets by their digit in every
+//      window (order[w][...] = set offsets grouped by digit);
+//   2. lane (w, d) adds its sets' sigma (mixed additions, bucket in VGPRs):
+//      ~span/16 additions per lane, the wave's lanes busy together;
+//   3. B <- d B by double-and-add (d <= 15), then a tree over the 16 digits
+//      of each window in LDS: S_w = sum_d d B_d;
+//   4. lane (w, 0): T_w = 2^(4w) S_w (4w doublings), then a tree over the
+//      windows: S_job = sum_w T_w; lane 0 converts to affine and writes the
+//      job code (first failing set code, signatures before pubkeys).
+// The dependent chain is ~max-bucket additions + 6 + 4 + 60 doublings + 4
+// additions + one inversion, against span + 30 + 75 sequential operations of
+// the (job, window)-lane form; 4 waves per job (4,096 at C4).  Invalid and
+// identity signatures add nothing (their job is rejected by its code).
+// S_job's affine value does not depend on the order of the additions.
+constexpr uint32_t MSM_LANES = 256;
+__global__ void __launch_bounds__(MSM_LANES, 1) k_msm_fused(dev_batch b, dev_work w) {
+  __shared__ g2j pts[MSM_LANES];             // tree exchange
+  __shared__ uint8_t order[16][256];         // set offsets by digit, per window
+  __shared__ uint32_t cnt[16][16], start[16][17];
+  const uint32_t j = blockIdx.x, tid = threadIdx.x, win = tid >> 4, dig = tid & 15u;
+  const uint32_t beg = b.job_off[j], end = b.job_off[j + 1];
+  g2j acc;
+  jac_set_inf(acc);
+  bool first = true;
+  // jobs are sorted and summed 256 sets at a time (block-sized jobs: once)
+  for (uint32_t c0 = beg; c0 < end; c0 += 256u) {
+    const uint32_t n = min(end - c0, 256u);
+    cnt[win][dig] = 0u;
+    __syncthreads();
+    // 1. digit histogram of every window (lane t takes set t)
+    const bool live = tid < n && w.sig_code[c0 + tid] == C_OK && !w.sig_inf[c0 + tid];
+    const uint64_t r = tid < n ? b.scalars[c0 + tid] : 0ull;
+    if (live)
+      for (uint32_t ww = 0; ww < 16; ww++) atomicAdd(&cnt[ww][(uint32_t)(r >> (4u * ww)) & 15u], 1u);
+    __syncthreads();
+    if (dig == 0) {
+      uint32_t a = 0;
+      for (uint32_t d = 0; d < 16; d++) { start[win][d] = a; a += cnt[win][d]; }
+      start[win][16] = a;
+    }
+    __syncthreads();
+    cnt[win][dig] = 0u;
+    __syncthreads();
+    if (live)
+      for (uint32_t ww = 0; ww < 16; ww++) {
+        const uint32_t d = (uint32_t)(r >> (4u * ww)) & 15u;
+        order[ww][start[ww][d] + atomicAdd(&cnt[ww][d], 1u)] = (uint8_t)tid;
+      }
+    __syncthreads();
+    // 2. bucket (win, dig): its sets' signatures (digit 0 contributes nothing)
+    if (dig != 0) {
+      const uint32_t k0 = start[win][dig], k1 = start[win][dig + 1];
+      for (uint32_t k = k0; k < k1; k++) {
+        const g2a s = w.sig_aff[c0 + order[win][k]];
+        if (first) jac_from_aff(acc, s);
+        else jac_add_aff(acc, acc, s);
+        first = false;
+      }
+    }
+    __syncthreads();  // order / start are rewritten by the next chunk
+  }
+  // 3. d B_d (MSB-first double-and-add), then the tree over the digits
+  if (dig > 1 && !jac_is_inf(acc)) {
+    const g2j base = acc;
+    const int top = 31 - __clz((int)dig);
+    for (int bit = top - 1; bit >= 0; bit--) {
+      jac_dbl(acc, acc);
+      if ((dig >> bit) & 1u) jac_add(acc, acc, base);
+    }
+  }
+  pts[tid] = acc;
+  __syncthreads();
+  for (uint32_t st = 8; st >= 1; st >>= 1) {
+    if (dig < st) {
+      g2j o = pts[tid + st];
+      jac_add(acc, acc, o);
+      pts[tid] = acc;
+    }
+    __syncthreads();
+  }
+  // 4. T_w = 2^(4 w) S_w, then the tree over the windows
+  if (dig == 0) {
+    for (uint32_t k = 0; k < 4u * win; k++) jac_dbl(acc, acc);
+    pts[tid] = acc;
+  }
+  __syncthreads();
+  for (uint32_t st = 8; st >= 1; st >>= 1) {
+    if (dig == 0 && win < st) {
+      g2j o = pts[tid + 16u * st];
+      jac_add(acc, acc, o);
+      pts[tid] = acc;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    g2a sa;
+    if (!jac_to_aff(sa, acc)) { sa.x = fp2_zero(); sa.y = fp2_zero(); }
+    w.s_aff[j] = sa;
+    w.s_inf[j] = jac_is_inf(acc) ? 1u : 0u;
+  }
+}
+
+// per job, after the pubkeys (ST_S_TREE, k_msm_fused mode): the job code
+// (first failing set, signatures before pubkeys, maybeBatch.ts:20-24); a
+// rejected job's S_job becomes the identity, so its (-G1, S_job) pair is 1
+__global__ void BGV_BULK k_job_code(dev_batch b, dev_work w) {
+  const uint32_t j = gtid();
+  if (j >= b.n_jobs) return;
+  const uint32_t beg = b.job_off[j], end = b.job_off[j + 1];
+  int32_t code = C_OK;
+  for (uint32_t i = beg; i < end && code == C_OK; i++) code = w.sig_code[i];
+  for (uint32_t i = beg; i < end && code == C_OK; i++) code = w.pk_code[i];
+  if (end == beg) code = C_EMPTY_JOB;
+  w.job_code[j] = code;
+  if (code != C_OK) {
+    g2a z;
+    z.x = fp2_zero();
+    z.y = fp2_zero();
+    w.s_aff[j] = z;
+    w.s_inf[j] = 1u;
+  }
+}
+
 // ------------------------------------------------------ per-job S tree
 // Sum of [r_i] sigma_i per job as a segmented pairwise tree: level `s`
 // folds element i + s into i for every i at an even multiple of s inside
@@ -1030,17 +1157,23 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       break;
     case ST_SIG_SCALE:
       if (b.split && !b.msm) break;  // [r_i] sigma_i already ran in k_sig_split
-      if (b.msm) {
+      if (b.msm == 2) {
         BGV_LAUNCH(k_msm_bucket, b.n_jobs * 16u, b, w);
+      } else if (b.msm) {
+        if (b.n_jobs) hipLaunchKernelGGL(k_msm_fused, dim3(b.n_jobs), dim3(MSM_LANES), 0, st, b, w);
       } else {
         BGV_LAUNCH(k_sig_scale, b.n_sets, b, w);
       }
       break;
     case ST_S_TREE:
       BGV_LAUNCH(k_set_job, b.n_jobs, b, w);
-      if (b.msm) {
+      if (b.msm == 2) {
         BGV_LAUNCH(k_msm_window, b.n_jobs * 16u, b, w);
         BGV_LAUNCH(k_msm_job, b.n_jobs, b, w);
+        break;
+      }
+      if (b.msm) {
+        BGV_LAUNCH(k_job_code, b.n_jobs, b, w);
         break;
       }
       for (uint32_t s = 1; s < span; s *= 2) BGV_LAUNCH(k_s_level, b.n_sets, b, w, s);

@@ -342,7 +342,7 @@ def test_signature_msm_bit_identical_to_per_set_scaling():
     byte-identical, and the golden verdicts hold in both modes."""
     from lodestar_amd import native
     outs = {}
-    for mode in ("0", "1"):
+    for mode in ("0", "1", "2"):
         d = native.Device(0, msm=int(mode))
         try:
             G.load_golden_table(d)
@@ -362,7 +362,7 @@ def test_signature_msm_bit_identical_to_per_set_scaling():
             outs[mode] = (part, ok, syn_part)
         finally:
             d.close()
-    assert outs["0"] == outs["1"]
+    assert outs["0"] == outs["1"] == outs["2"]
 
 
 @pytest.mark.gpu
