@@ -100,7 +100,7 @@ struct bgv_ctx {
   dev_work part_w;
   // bgv_debug_stages
   dbuf<g1a> pk_agg;
-  dbuf<fp12_t> dbg_fe;
+  dbuf<fp12_t> dbg_fe, dbg_f;
   dbuf<uint8_t> dbg_out;
   dbuf<uint64_t> scalars;
   dbuf<g1a> raw_conv;
@@ -227,7 +227,7 @@ int bgv_close(bgv_ctx* c) {
   c->sk.release();
   c->stage_dev.release();
   c->raw_in.release(); c->gen_out.release(); c->pk_tmp.release(); c->pk_codes.release();
-  c->pk_agg.release(); c->dbg_fe.release(); c->dbg_out.release();
+  c->pk_agg.release(); c->dbg_fe.release(); c->dbg_f.release(); c->dbg_out.release();
   c->scalars.release(); c->raw_conv.release();
   c->sig_aff.release(); c->h_aff.release(); c->sig_inf.release(); c->flags.release();
   c->sig_code.release(); c->pk_code.release(); c->job_code.release(); c->job_result.release(); c->set_code.release();
@@ -511,6 +511,16 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   // Miller loop moves to the hash stream, phase 1 (C4 40.4 -> 39.5 ms); with
   // one pair per item it loses (C4/2 26.4 -> 28.5 ms)
   d.lines = (uint32_t)(!d.split && !d.miller_coop && (k.lines >= 0 ? k.lines : d.pairs_per_item == 2));
+  // the lines take 3 x 68 Fp2 = 19.6 KB per set (1.97 GB at C4, 2.6 GB at the
+  // Node pool's 2^17-set batch cap): kept only while a quarter of the free HBM
+  // covers them, else the loop recomputes them (miller_loop2, same values)
+  if (d.lines) {
+    const size_t need = (size_t)3 * MILLER_STEPS * n * sizeof(fp2_t);
+    size_t free_b = 0, total_b = 0;
+    if (need > c->lines.cap * sizeof(fp2_t) &&
+        (hipMemGetInfo(&free_b, &total_b) != hipSuccess || need > free_b / 4))
+      d.lines = 0;
+  }
   d.job_lanes = k.job_lanes ? (uint32_t)k.job_lanes : 36u;
   if (b->scalars && !b->on_device) {
     // staged with the other host arrays above
@@ -562,6 +572,8 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
   if (d.lines) {
     if ((r = c->lines.ensure((size_t)3 * MILLER_STEPS * ns))) return r;
     w.lines = c->lines.p;
+  } else if (c->lines.cap) {
+    c->lines.release();  // a batch without lines: give the 19.6 KB per set back
   }
   w.msm_bucket = nullptr; w.msm_mask = nullptr; w.msm_win = nullptr;
   if (d.msm == 2) {
@@ -829,11 +841,18 @@ int bgv_debug_stages(bgv_ctx* c, const bgv_batch* b, int32_t* job_result, int32_
   const uint32_t n = d.n_sets, J = d.n_jobs;
   if (int r = c->pk_agg.ensure(n ? n : 1)) return r;
   w.pk_agg = c->pk_agg.p;
-  if (int r = run_stages(c, d, w, 0, ST_COUNT)) return r;
+  // the Miller values are copied before the product tree, which folds groups
+  // of them in place (k_job_prefold, k_f_level); deferred subgroup verdicts
+  // are applied first (idempotent: the tree stage applies them again)
+  if (int r = run_stages(c, d, w, 0, ST_F_TREE)) return r;
+  if (d.defer_grp) launch_sig_fixup(c->st, d, w);
+  if (int r = c->dbg_f.ensure((size_t)n + J + 1)) return r;
+  if (n + J) HIPCHK(hipMemcpyAsync(c->dbg_f.p, w.f_set, (size_t)(n + J) * sizeof(fp12_t), hipMemcpyDeviceToDevice, c->st));
+  if (int r = run_stages(c, d, w, ST_F_TREE, ST_COUNT)) return r;
   // final exponentiations of every Miller value, job product and the batch product
   const uint32_t n_fe = n + 2 * J + 1;
   if (int r = c->dbg_fe.ensure(n_fe)) return r;
-  launch_final_exp_many(c->st, w.f_set, c->dbg_fe.p, n + J);
+  launch_final_exp_many(c->st, c->dbg_f.p, c->dbg_fe.p, n + J);
   launch_final_exp_many(c->st, w.f_job, c->dbg_fe.p + n + J, J);
   if (J) launch_final_exp_many(c->st, w.f_batch, c->dbg_fe.p + n + 2 * J, 1);
   launch_fp12_convert(c->st, c->dbg_fe.p, c->dbg_fe.p, n_fe, false);

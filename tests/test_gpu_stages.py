@@ -110,3 +110,33 @@ def test_stage_values_independent_of_batching(golden):
             first += k
     finally:
         d.close()
+
+
+def test_debug_pair_values_before_the_product_tree():
+    """bgv_debug_stages' pair values are every pair's own Miller value even when
+    the two-level job fold (k_job_prefold, default for <= 256 jobs of 64-256
+    sets, e.g. one C2 gossip batch) folds groups of them in place: identical
+    with the fold on and off, and their product is the job's value (1 for a
+    valid job)."""
+    from lodestar_amd import native
+    from tests.test_gpu_parity import _synthetic_on
+    outs = {}
+    for prefold in (0, 1):
+        d = native.Device(0, prefold=prefold)
+        try:
+            d.gen_keys(0, 512, 5)
+            a, bad = _synthetic_on(d, 64, 8, 0, 512, 21)
+            a["n_jobs"] = 1
+            a["job_offsets"] = np.array([0, 64], np.uint32)
+            out = d.debug_stages(a)
+            assert out["job_result"].tolist() == [1]
+            assert d.last_stats.layout() is not None
+            outs[prefold] = out
+        finally:
+            d.close()
+    assert (outs[0]["pair_fe"] == outs[1]["pair_fe"]).all()
+    prod = B.F12_ONE
+    for k in range(65):  # 64 set pairs and the job's (-G1, S_job) pair
+        prod = B.f12_mul(prod, _flat(outs[1]["pair_fe"][k].tobytes()))
+    assert B.f12_eq(prod, _flat(outs[1]["job_fe"][0].tobytes()))
+    assert B.f12_eq(prod, B.F12_ONE)
