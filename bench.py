@@ -53,8 +53,10 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def build_segment(blocks: list[int], seed: int = SEED, att_per_block: int = ATT_PER_BLOCK):
-    """Host arrays for the given block ids of the segment (deterministic per block)."""
+def build_segment(blocks: list[int], seed: int = SEED, att_per_block: int = ATT_PER_BLOCK, att_k: int = ATT_K):
+    """Host arrays for the given block ids of the segment (deterministic per
+    block): att_per_block attestation aggregates of att_k pubkeys, the sync
+    aggregate (512) and two singles per block."""
     job_off, pk_off, idx, msgs = [0], [0], [], []
     per_block = att_per_block + SETS_PER_BLOCK - ATT_PER_BLOCK
     perm = np.random.default_rng(seed).permutation(N_VALIDATORS).astype(np.uint32)
@@ -63,12 +65,12 @@ def build_segment(blocks: list[int], seed: int = SEED, att_per_block: int = ATT_
         rng = np.random.default_rng([seed, b])
         # attesters of the block: disjoint committees (a slice of a shuffling)
         start = int(rng.integers(0, N_VALIDATORS))
-        att = np.take(perm, np.arange(start, start + att_per_block * ATT_K) % N_VALIDATORS)
+        att = np.take(perm, np.arange(start, start + att_per_block * att_k) % N_VALIDATORS)
         sync = rng.choice(N_VALIDATORS, size=SYNC_K, replace=False).astype(np.uint32)
         singles = rng.integers(0, N_VALIDATORS, size=2).astype(np.uint32)
         for a in range(att_per_block):
-            idx.append(att[a * ATT_K : (a + 1) * ATT_K])
-            pk_off.append(pk_off[-1] + ATT_K)
+            idx.append(att[a * att_k : (a + 1) * att_k])
+            pk_off.append(pk_off[-1] + att_k)
         idx.append(sync)
         pk_off.append(pk_off[-1] + SYNC_K)
         for s in singles:
@@ -270,6 +272,9 @@ def small_configs(d, torch, dev, arrays):
     # C3: one block = 128 attestation aggregates (k=128) + sync (k=512) + 2 singles, one job
     c3a = signed(d, build_segment([0], seed=SEED + 2000, att_per_block=128))
     out["c3_block_latency_ms"] = {"p50": p50_latency(d, c3a), "sets": c3a["n_sets"], "pubkey_refs": int(c3a["pk_offsets"][-1])}
+    # C3 at 1M validators: attestations carry ~90% of a 488-member committee (k = 440)
+    c3b = signed(d, build_segment([0], seed=SEED + 2500, att_per_block=128, att_k=440))
+    out["c3_block_k440_latency_ms"] = {"p50": p50_latency(d, c3b), "sets": c3b["n_sets"], "pubkey_refs": int(c3b["pk_offsets"][-1])}
     # C1: 128 single sets, one job
     out["c1_singles_latency_ms"] = {"p50": p50_latency(d, signed(d, singles(128, SEED + 3000))), "sets": 128}
     # one set (verifyOnMainThread gossip block proposer, chain/validation/block.ts:146)
@@ -293,6 +298,18 @@ def small_configs(d, torch, dev, arrays):
                             "jobs_false": int((c5_expect == 0).sum()), "jobs_rejected": int((c5_expect < 0).sum()),
                             "verdicts_match_expected": ok5, "batch_retries": int(d.last_stats.batch_retries)}
     return out
+
+
+def epoch_slice(d, torch, dev, arrays_host: dict, sigs, blocks: int = 32, reps: int = 7):
+    """One epoch of the segment (32 blocks = 3,136 sets): the batch a range
+    sync hands the verifier per epoch (sync/constants.ts:41), on device, p50"""
+    from lodestar_amd.dist import select_jobs
+    sub = select_jobs(dict(arrays_host, sigs=sigs), list(range(blocks)))
+    da = to_device(sub, torch, dev)
+    da.update(sig_len=torch.full((sub["n_sets"],), 96, dtype=torch.int32, device=dev), scalars=None)
+    p50 = p50_latency(d, da, reps=reps, on_device=True)
+    return {"sets": int(sub["n_sets"]), "blocks": blocks, "p50_ms": p50, "sets_per_s": round(sub["n_sets"] / p50 * 1e3, 1),
+            "layout": d.last_stats.layout()}
 
 
 def host_resident_c4(d, arrays_host: dict, reps: int = 3):
@@ -492,6 +509,7 @@ def main():
         host["sig_len"] = np.full(n_sets, 96, np.uint32)
         host["scalars"] = None
         legs["c4_host_resident"] = host_resident_c4(d, host)
+        legs["c4_epoch_slice"] = epoch_slice(d, torch, dev, arrays, host["sigs"])
         if world == 1:
             legs["strong_shard_projection"] = shard_projection(d, torch, dev, host)
 

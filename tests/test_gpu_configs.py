@@ -129,10 +129,11 @@ def test_c2_gossip_batch(big):
         asyncio.run(pool.close())
 
 
-@pytest.mark.parametrize("coalesce", [False, True])
-def test_c3_blocks_first_invalid(coalesce):
-    """C3: verifyBlocksSignatures over 3 blocks of 131 sets (128 x k=128 +
-    sync k=512 + 2 singles); block 1 has one wrong-message attestation"""
+@pytest.mark.parametrize("coalesce,att_k", [(False, 128), (True, 128), (True, 440)])
+def test_c3_blocks_first_invalid(coalesce, att_k):
+    """C3: verifyBlocksSignatures over 3 blocks of 131 sets (128 x k=att_k +
+    sync k=512 + 2 singles; k = 440 is ~90% of a 488-member committee at 1M
+    validators); block 1 has one wrong-message attestation"""
     from lodestar_amd import verifier as V
     pool = V.BlsGpuVerifier(devices=(0,))
     try:
@@ -140,8 +141,8 @@ def test_c3_blocks_first_invalid(coalesce):
         d.gen_keys(0, N_TABLE, SEED)
         blocks = []
         for b in range(3):
-            a = bench.build_segment([b], seed=SEED + 2000, att_per_block=128)
-            assert a["n_sets"] == 131 and int(a["pk_offsets"][-1]) == 128 * 128 + 512 + 2
+            a = bench.build_segment([b], seed=SEED + 2000, att_per_block=128, att_k=att_k)
+            assert a["n_sets"] == 131 and int(a["pk_offsets"][-1]) == 128 * att_k + 512 + 2
             sign_msgs = a["msgs"].copy()
             if b == 1:
                 sign_msgs[40, 0] ^= 1
