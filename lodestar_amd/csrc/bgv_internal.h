@@ -93,6 +93,27 @@ enum Stage {
   ST_COUNT
 };
 
+#ifdef __HIPCC__
+BGV_HD bool g1a_is_zero(const g1a& p) { return fp_is_zero(p.x) && fp_is_zero(p.y); }
+
+// row of the pubkey table (or of the raw side table for bit 31); an index
+// past either flags range_err and yields the identity
+__device__ __forceinline__ void load_pk(g1a& out, const dev_batch& b, uint32_t idx, bool& range_err) {
+  if (idx & 0x80000000u) {
+    const uint32_t r = idx & 0x7fffffffu;
+    if (r >= b.n_raw) { range_err = true; fp_set_zero(out.x); fp_set_zero(out.y); return; }
+    out = b.raw_pks[r];
+  } else {
+    if (idx >= b.table_n) { range_err = true; fp_set_zero(out.x); fp_set_zero(out.y); return; }
+    out = b.table[idx];
+  }
+}
+#endif
+
+// keys per chunk of the balanced pubkey gather (k_pk_chunk)
+constexpr uint32_t PK_CHUNK = 32;
+
+void launch_pk_gather(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_gather.hip
 void launch_raw_pks(hipStream_t st, const uint8_t* raw, g1a* out, uint32_t n);
 void launch_table_from_compressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n, int32_t* codes);
 void launch_table_from_uncompressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n, int32_t* codes);

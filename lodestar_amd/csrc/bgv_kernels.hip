@@ -78,19 +78,6 @@ namespace bgv {
 __device__ __forceinline__ uint32_t gtid() { return blockIdx.x * blockDim.x + threadIdx.x; }
 
 // ---------------------------------------------------------------- helpers
-BGV_HD bool g1a_is_zero(const g1a& p) { return fp_is_zero(p.x) && fp_is_zero(p.y); }
-
-__device__ __forceinline__ void load_pk(g1a& out, const dev_batch& b, uint32_t idx, bool& range_err) {
-  if (idx & 0x80000000u) {
-    const uint32_t r = idx & 0x7fffffffu;
-    if (r >= b.n_raw) { range_err = true; fp_set_zero(out.x); fp_set_zero(out.y); return; }
-    out = b.raw_pks[r];
-  } else {
-    if (idx >= b.table_n) { range_err = true; fp_set_zero(out.x); fp_set_zero(out.y); return; }
-    out = b.table[idx];
-  }
-}
-
 // ------------------------------------------------------------ k_raw_pks
 // uncompressed 96 B big-endian, trusted (multithread/worker.ts:108-114:
 // PublicKey.fromBytes(.., affine) without validation); infinity -> (0, 0)
@@ -373,7 +360,6 @@ __global__ void __launch_bounds__(64, BGV_HASH_WAVES) k_hash(dev_batch b, dev_wo
 // a 128-key attestation 4, a single 1) so lanes of one wave do equal work;
 // chunk offsets come from a device scan.  Then one lane per set folds its
 // chunk sums, applies the batch scalar r_i and converts to affine.
-constexpr uint32_t PK_CHUNK = 32;
 
 // Offsets that run backwards (an on-device batch that breaks the contract;
 // host batches are checked by the library) give the set no chunks, and the
@@ -428,31 +414,8 @@ __global__ void BGV_BULK k_chunk_set(dev_batch b, dev_work w) {
   for (uint32_t c = w.chunk_off[i]; c < end; c++) w.chunk_set[c] = i;
 }
 
-#ifndef BGV_PKC_WAVES
-#define BGV_PKC_WAVES BGV_PK_WAVES
-#endif
-__global__ void __launch_bounds__(64, BGV_PKC_WAVES) k_pk_chunk(dev_batch b, dev_work w) {
-  const uint32_t g = gtid();
-  if (g >= min(w.chunk_off[b.n_sets], b.chunk_bound)) return;
-  const uint32_t i = w.chunk_set[g];
-  const uint32_t beg = b.pk_off[i] + (g - w.chunk_off[i]) * PK_CHUNK;
-  const uint32_t end = min(beg + PK_CHUNK, b.pk_off[i + 1]);
-  g1j acc;
-  jac_set_inf(acc);
-  bool range_err = false;
-  for (uint32_t k = beg; k < end; k++) {
-    g1a p;
-    load_pk(p, b, b.pk_idx[k], range_err);
-    if (g1a_is_zero(p)) continue;  // infinity entry adds nothing
-    jac_add_aff(acc, acc, p);
-  }
-  if (range_err) {  // marker (X, Y, Z) = (0, 1, 1): not on E1, never produced by point additions
-    fp_set_zero(acc.x);
-    acc.y = FP_ONE;
-    acc.z = FP_ONE;
-  }
-  w.pk_part[g] = acc;
-}
+// k_pk_chunk (the gather) lives in bgv_gather.hip: it runs with the product
+// inlined, so the next row's load stays in flight across the additions
 
 __global__ void __launch_bounds__(64, BGV_PK_WAVES) k_pk(dev_batch b, dev_work w) {
   const uint32_t i = gtid();
@@ -602,8 +565,9 @@ __global__ void BGV_BULK k_msm_job(dev_batch b, dev_work w) {
 // identity signatures add nothing (their job is rejected by its code).
 // S_job's affine value does not depend on the order of the additions.
 constexpr uint32_t MSM_LANES = 256;
-__global__ void __launch_bounds__(MSM_LANES, 1) k_msm_fused(dev_batch b, dev_work w) {
-  __shared__ g2j pts[MSM_LANES];             // tree exchange
+__global__ void __launch_bounds__(MSM_LANES, 1) k_msm_fused(dev_batch b, dev_work w, uint32_t chunk) {
+  __shared__ g2j pts[128];                   // tree exchange (8 slots per window)
+  extern __shared__ g2a sg[];                // the chunk's decoded signatures (dynamic: chunk x 192 B)
   __shared__ uint8_t order[16][256];         // set offsets by digit, per window
   __shared__ uint32_t cnt[16][16], start[16][17];
   const uint32_t j = blockIdx.x, tid = threadIdx.x, win = tid >> 4, dig = tid & 15u;
@@ -611,14 +575,17 @@ __global__ void __launch_bounds__(MSM_LANES, 1) k_msm_fused(dev_batch b, dev_wor
   g2j acc;
   jac_set_inf(acc);
   bool first = true;
-  // jobs are sorted and summed 256 sets at a time (block-sized jobs: once)
-  for (uint32_t c0 = beg; c0 < end; c0 += 256u) {
-    const uint32_t n = min(end - c0, 256u);
+  // jobs are sorted and summed `chunk` (<= 256) sets at a time (block-sized jobs: once)
+  for (uint32_t c0 = beg; c0 < end; c0 += chunk) {
+    const uint32_t n = min(end - c0, chunk);
     cnt[win][dig] = 0u;
     __syncthreads();
     // 1. digit histogram of every window (lane t takes set t)
     const bool live = tid < n && w.sig_code[c0 + tid] == C_OK && !w.sig_inf[c0 + tid];
     const uint64_t r = tid < n ? b.scalars[c0 + tid] : 0ull;
+    // staged in LDS: the bucket additions below then wait on LDS, not HBM
+    // (every product call begins with s_waitcnt on all outstanding loads)
+    if (live) sg[tid] = w.sig_aff[c0 + tid];
     if (live)
       for (uint32_t ww = 0; ww < 16; ww++) atomicAdd(&cnt[ww][(uint32_t)(r >> (4u * ww)) & 15u], 1u);
     __syncthreads();
@@ -640,7 +607,7 @@ __global__ void __launch_bounds__(MSM_LANES, 1) k_msm_fused(dev_batch b, dev_wor
     if (dig != 0) {
       const uint32_t k0 = start[win][dig], k1 = start[win][dig + 1];
       for (uint32_t k = k0; k < k1; k++) {
-        const g2a s = w.sig_aff[c0 + order[win][k]];
+        const g2a s = sg[order[win][k]];
         if (first) jac_from_aff(acc, s);
         else jac_add_aff(acc, acc, s);
         first = false;
@@ -657,27 +624,25 @@ __global__ void __launch_bounds__(MSM_LANES, 1) k_msm_fused(dev_batch b, dev_wor
       if ((dig >> bit) & 1u) jac_add(acc, acc, base);
     }
   }
-  pts[tid] = acc;
-  __syncthreads();
+  // level st: digits [st, 2 st) hand their sums to digits [0, st)
   for (uint32_t st = 8; st >= 1; st >>= 1) {
+    if (dig >= st && dig < 2u * st) pts[8u * win + dig - st] = acc;
+    __syncthreads();
     if (dig < st) {
-      g2j o = pts[tid + st];
+      g2j o = pts[8u * win + dig];
       jac_add(acc, acc, o);
-      pts[tid] = acc;
     }
     __syncthreads();
   }
   // 4. T_w = 2^(4 w) S_w, then the tree over the windows
-  if (dig == 0) {
+  if (dig == 0)
     for (uint32_t k = 0; k < 4u * win; k++) jac_dbl(acc, acc);
-    pts[tid] = acc;
-  }
-  __syncthreads();
   for (uint32_t st = 8; st >= 1; st >>= 1) {
+    if (dig == 0 && win >= st && win < 2u * st) pts[win - st] = acc;
+    __syncthreads();
     if (dig == 0 && win < st) {
-      g2j o = pts[tid + 16u * st];
+      g2j o = pts[win];
       jac_add(acc, acc, o);
-      pts[tid] = acc;
     }
     __syncthreads();
   }
@@ -1150,7 +1115,7 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       }
       break;
     case ST_PK:  // after launch_prep: the gather from the HBM table
-      BGV_LAUNCH(k_pk_chunk, b.chunk_bound, b, w);
+      launch_pk_gather(st, b, w);  // bgv_gather.hip
       break;
     case ST_PK_SCALE:
       BGV_LAUNCH(k_pk, b.n_sets, b, w);
@@ -1160,7 +1125,10 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       if (b.msm == 2) {
         BGV_LAUNCH(k_msm_bucket, b.n_jobs * 16u, b, w);
       } else if (b.msm) {
-        if (b.n_jobs) hipLaunchKernelGGL(k_msm_fused, dim3(b.n_jobs), dim3(MSM_LANES), 0, st, b, w);
+        if (b.n_jobs) {
+          const uint32_t chunk = 1u << min(b.span_log2, 8u);  // LDS for one chunk of signatures
+          hipLaunchKernelGGL(k_msm_fused, dim3(b.n_jobs), dim3(MSM_LANES), chunk * sizeof(g2a), st, b, w, chunk);
+        }
       } else {
         BGV_LAUNCH(k_sig_scale, b.n_sets, b, w);
       }

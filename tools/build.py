@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "lodestar_amd", "csrc")
 LIB = os.path.join(ROOT, "lodestar_amd", "libbgv.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["bgv_kernels.hip", "bgv_miller.hip", "bgv_latency.hip", "bgv_tail.hip", "bgv_api.hip"]
+SOURCES = ["bgv_kernels.hip", "bgv_miller.hip", "bgv_latency.hip", "bgv_tail.hip", "bgv_gather.hip", "bgv_api.hip"]
 
 
 def deps():
