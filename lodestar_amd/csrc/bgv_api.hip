@@ -478,9 +478,13 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   const bgv_cfg& k = c->cfg;
   d.pairs_per_item = k.pairs ? (uint32_t)k.pairs : (n >= PAIRS2_MIN ? 2u : 1u);
   d.split = k.split >= 0 ? (uint32_t)k.split : (n < SPLIT_MAX ? 1u : 0u);
-  // sum r_i sigma_i per job by a bucket MSM (16 x 4-bit windows, one
-  // workgroup per job, k_msm_fused) when jobs are block-sized (<= 256 sets)
-  d.msm = k.msm >= 0 ? (uint32_t)k.msm : ((n >= MSM_MIN && d.span_log2 <= 8) ? 1u : 0u);
+  // sum r_i sigma_i per job by a bucket MSM (16 x 4-bit windows) when jobs
+  // are block-sized (<= 256 sets).  The latency mode takes the fused kernel
+  // (one workgroup per job, k_msm_fused: short chain, many idle lanes); bulk
+  // batches the (job, window)-lane kernels, which do a third of its SIMD-time
+  // (C4: k_msm_fused 49 ms beside the hash, pubkeys and Miller loops,
+  // stretching the Miller kernel from 14.5 to 26.4 ms, r03 trace)
+  d.msm = k.msm >= 0 ? (uint32_t)k.msm : ((n >= MSM_MIN && d.span_log2 <= 8) ? (d.split ? 1u : 2u) : 0u);
   // Deferred subgroup checks: the signature stage only decodes, and the checks
   // of sets [defer_from, n) run beside the Miller loops (bgv_kernels.hip
   // k_job_recode).  Wherever the MSM sums the signatures (the latency mode

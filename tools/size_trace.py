@@ -57,23 +57,22 @@ def run(sizes, reps):
 
 
 def analyze(path, calls_path):
+    """the timeline of the last call of every size: the dispatches after the
+    previous call's batch final exponentiation up to this call's (one
+    k_batch_final per verify call; the signing calls have none)"""
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     calls = json.load(open(calls_path))
-    starts = [k for k, r in enumerate(rows) if "k_gen_scalars" in r["Kernel_Name"]]
-    starts = starts[-len(calls):]
+    bf = [r for r in rows if "k_batch_final" in r["Kernel_Name"]][-len(calls):]
     for ci, n in enumerate(calls):
-        if ci + 1 < len(calls) and calls[ci + 1] == n:
+        if ci == 0 or (ci + 1 < len(calls) and calls[ci + 1] == n):
             continue  # only the last call of each size
-        lo = starts[ci]
-        hi = starts[ci + 1] if ci + 1 < len(starts) else len(rows)
-        sel = rows[lo:hi]
-        # drop the next call's leading copies
+        t_prev, t_end = int(bf[ci - 1]["End_Timestamp"]), int(bf[ci]["End_Timestamp"])
+        sel = [r for r in rows if t_prev < int(r["Start_Timestamp"]) and int(r["End_Timestamp"]) <= t_end]
         t0 = int(sel[0]["Start_Timestamp"])
-        t_end = max(int(r["End_Timestamp"]) for r in sel)
-        print(f"== {n} sets: device span {(t_end - t0) / 1e6:.3f} ms")
+        print(f"== {n} sets: device span {(t_end - t0) / 1e6:.3f} ms (first dispatch to the final exponentiation's end)")
         for r in sel:
-            s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-            print(f"  {(s - t0) / 1e6:8.3f} {(e - t0) / 1e6:8.3f} {(e - s) / 1e6:8.3f} q{r['Queue_Id']} "
+            s_, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            print(f"  {(s_ - t0) / 1e6:8.3f} {(e - t0) / 1e6:8.3f} {(e - s_) / 1e6:8.3f} q{r['Queue_Id']} "
                   f"{r['Kernel_Name'][:40]:40s} grid={r['Grid_Size_X']} vgpr={r.get('VGPR_Count', '')}/"
                   f"{r.get('Accum_VGPR_Count', '')} lds={r.get('LDS_Block_Size', '')} scr={r.get('Scratch_Size', '')}")
 
