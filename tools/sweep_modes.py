@@ -35,6 +35,10 @@ MODES = {  # bgv_cfg overrides (include/bgv.h)
     "j18": {"job_lanes": 18},
     "j6": {"job_lanes": 6},
     "timed": {"timing": 1},
+    "msm0": {"msm": 0},
+    "msm1": {"msm": 1},
+    "msm2": {"msm": 2},
+    "nodefer": {"defer_pct": 0},
 }
 
 
