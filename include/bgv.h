@@ -155,7 +155,7 @@ typedef struct bgv_stats {
 typedef struct bgv_cfg {
   uint32_t struct_size; /* sizeof(bgv_cfg) */
   int32_t split;        /* -1 auto; 0 bulk kernels; 1 latency mode (two-lane hash maps, cooperative G2) */
-  int32_t miller;       /* -1 auto; 1 one-lane set-pair loop; 6 / 18 / 36 lanes per pair (cooperative) */
+  int32_t miller;       /* -1 auto; 1 one-lane set-pair loop; 2 two-lane loop; 6 / 18 / 36 lanes per pair (cooperative) */
   int32_t job_lanes;    /* 0 auto (36); 6 / 18 / 36: lanes of the per-job (-G1, S_job) pairs */
   int32_t msm;          /* -1 auto; 0 per-set [r_i] sigma_i + tree; 1 per-job bucket MSM (one workgroup per job); 2 the (job, window)-lane MSM (A/B) */
   int32_t pairs;        /* 0 auto; 1 / 2 pairs per one-lane Miller work item */

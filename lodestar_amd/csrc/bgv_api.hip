@@ -174,7 +174,7 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
     if (cfg->struct_size != sizeof k) return fail(BGV_E_INVALID_ARG, "bgv_cfg.struct_size %u, expected %zu", cfg->struct_size, sizeof k);
     k = *cfg;
     auto lanes_ok = [](int v) { return v == 6 || v == 18 || v == 36; };
-    if (k.miller != -1 && k.miller != 1 && !lanes_ok(k.miller)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.miller %d", k.miller);
+    if (k.miller != -1 && k.miller != 1 && k.miller != 2 && !lanes_ok(k.miller)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.miller %d", k.miller);
     if (k.job_lanes != 0 && !lanes_ok(k.job_lanes)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.job_lanes %d", k.job_lanes);
     if (k.pairs < 0 || k.pairs > 2) return fail(BGV_E_INVALID_ARG, "bgv_cfg.pairs %d", k.pairs);
     if (k.msm < -1 || k.msm > 2) return fail(BGV_E_INVALID_ARG, "bgv_cfg.msm %d", k.msm);

@@ -18,8 +18,8 @@ struct dev_batch {
   uint32_t n_sets, n_jobs, n_raw, table_n;
   uint32_t span_log2;    // per-job reduction tree covers 2^span_log2 sets
   uint32_t chunk_bound;  // upper bound of pubkey chunks (grid of k_pk_chunk)
-  uint32_t miller_coop;     // set pairs: 0 one-lane Miller loop (k_miller), else lanes per pair of the
-                            // cooperative loop (miller_coop.h: 6, 18 or 36)
+  uint32_t miller_coop;     // set pairs: 0 one-lane Miller loop (k_miller), 2 the two-lane loop
+                            // (k_miller_duo), else lanes per pair of the cooperative loop (miller_coop.h: 6, 18 or 36)
   uint32_t job_lanes;       // (-G1, S_job) pairs: lanes per pair of the cooperative loop (6, 18 or 36)
   uint32_t pairs_per_item;  // Miller pairs sharing one accumulator (1, or 2 for batches that fill the GPU)
   uint32_t msm;             // 1: per-job bucket MSM for sum r_i sigma_i (k_msm_*), 0: per-set [r_i] sigma_i + tree
@@ -123,6 +123,7 @@ void launch_prep(hipStream_t st, const dev_batch& b, const dev_work& w);  // bef
 void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work& w);
 void launch_miller(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_miller.hip
 void launch_lines(hipStream_t st, const dev_batch& b, const dev_work& w);   // bgv_miller.hip
+void launch_miller_duo(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_miller.hip
 void launch_sig_check(hipStream_t st, const dev_batch& b, const dev_work& w);   // subgroup checks only (sig_grp)
 void launch_sig_fixup(hipStream_t st, const dev_batch& b, const dev_work& w);   // k_sig_fix + k_job_recode
 void launch_sig_split_coop(hipStream_t st, const dev_batch& b, const dev_work& w);   // bgv_latency.hip

@@ -1148,6 +1148,10 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       BGV_LAUNCH(k_job_s, b.n_jobs, b, w, span);
       break;
     case ST_MILLER:  // (r_i PK_i, H(m_i)) pairs: needs ST_HASH and ST_PK only
+      if (b.miller_coop == 2) {
+        launch_miller_duo(st, b, w);  // bgv_miller.hip
+        break;
+      }
       if (b.miller_coop) {
         if (b.n_sets)
           launch_miller_coop(st, b.miller_coop, b, w, 0u, b.n_sets);

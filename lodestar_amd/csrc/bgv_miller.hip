@@ -35,6 +35,7 @@
 #define BGV_STEP_INLINE BGV_MILLER_STEP_INLINE
 #endif
 #include "bgv_internal.h"
+#include "miller_duo.h"
 
 namespace bgv {
 
@@ -77,6 +78,36 @@ __global__ void __launch_bounds__(64, BGV_MILLER_WAVES) k_miller(dev_batch b, de
     else miller_loop(f, ng, false, w.s_aff[j], false);
     w.f_set[b.n_sets + j] = f;
   }
+}
+
+// Two lanes per pair (miller_duo.h), 32 pairs per wave: pair t < n_sets is
+// (r_t PK_t, H(m_t)); a pair whose pubkey was rejected contributes 1.  For
+// batches between the cooperative layouts' reach and the one-lane loop's
+// (prepare(): ~6,000 to 35,000 sets), where one lane per pair leaves most
+// SIMDs idle and six lanes per pair oversubscribe them.
+__global__ void __launch_bounds__(64, 1) k_miller_duo(dev_batch b, dev_work w, uint32_t count) {
+  __shared__ duo_x_t sx[32];
+  const uint32_t lane = threadIdx.x, pr = lane >> 1, h = lane & 1u;
+  const uint32_t t = blockIdx.x * 32u + pr;
+  if (t >= count) return;  // both lanes of a pair leave together
+  if (w.pk_code[t] != C_OK) {  // rejected job: its Miller values are never used
+    fp6_t v;
+    if (h) fp6_zero(v);
+    else fp6_one(v);
+    if (h) w.f_set[t].c1 = v;
+    else w.f_set[t].c0 = v;
+    return;
+  }
+  const g1a P = w.rpk_aff[t];
+  const g2a Q = w.h_aff[t];
+  fp6_t fh;
+  duo_miller(fh, P, Q, h, sx[pr]);
+  if (h) w.f_set[t].c1 = fh;
+  else w.f_set[t].c0 = fh;
+}
+
+void launch_miller_duo(hipStream_t st, const dev_batch& b, const dev_work& w) {
+  if (b.n_sets) hipLaunchKernelGGL(k_miller_duo, dim3((b.n_sets + 31u) / 32u), dim3(64), 0, st, b, w, b.n_sets);
 }
 
 // the unevaluated lines of every set's H(m) (pairing.h miller_lines), on the

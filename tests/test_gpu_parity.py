@@ -221,12 +221,13 @@ def test_microbench_runs(dev):
 
 def test_cooperative_miller_bit_identical_to_serial():
     """The cooperative Miller loop (miller_coop.h) in its three layouts (36,
-    6 and 18 lanes per pair) and the one-lane loop (pairing.h, bgv_cfg.miller = 1)
+    6 and 18 lanes per pair), the two-lane loop (miller_duo.h) and the
+    one-lane loop (pairing.h, bgv_cfg.miller = 1)
     produce the same Fp12 batch partial, byte for byte, and the same verdicts."""
     from lodestar_amd import native
     outs = {}
-    for mode in ("serial", "coop", "6", "18"):
-        d = native.Device(0, miller={"serial": 1, "coop": 36, "6": 6, "18": 18}[mode])
+    for mode in ("serial", "coop", "6", "18", "duo"):
+        d = native.Device(0, miller={"serial": 1, "coop": 36, "6": 6, "18": 18, "duo": 2}[mode])
         try:
             G.load_golden_table(d)
             a, expected, _ = G.golden_arrays([0, 1, 9, 11, 12, 13], scalars_seed=3)

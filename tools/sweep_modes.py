@@ -27,6 +27,7 @@ MODES = {  # bgv_cfg overrides (include/bgv.h)
     "coop_msm": {"msm": 1},
     "split1_serial": {"split": 1, "miller": 1, "msm": 0},
     "split1_coop_msm": {"split": 1, "miller": 36, "msm": 1},
+    "m2": {"miller": 2},
     "m6": {"miller": 6},
     "m18": {"miller": 18},
     "m36": {"miller": 36},
