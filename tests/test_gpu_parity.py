@@ -240,7 +240,7 @@ def test_cooperative_miller_bit_identical_to_serial():
             outs[mode] = (part, ok, jr.tolist(), jr2.tolist(), bad)
         finally:
             d.close()
-    for mode in ("coop", "6", "18"):  # 36, 6 and 18 lanes per pair
+    for mode in ("coop", "6", "18", "duo"):  # 36, 6, 18 and 2 lanes per pair
         assert outs["serial"][0] == outs[mode][0], mode
         assert outs["serial"][1:4] == outs[mode][1:4], mode
     assert outs["coop"][2] == G.golden_arrays()[1]
