@@ -147,6 +147,7 @@ typedef struct bgv_stats {
   uint32_t msm;                 /* 1: per-job bucket MSM for sum r_i sigma_i */
   uint32_t lines;               /* 1: fixed-argument Miller lines */
   uint32_t defer_from;          /* subgroup checks of sets >= defer_from run beside the Miller loops (n_sets: none) */
+  uint32_t clear_lanes;         /* latency mode: lanes per point of the cofactor clearing */
 } bgv_stats;
 
 /* Pipeline overrides for tests and A/B tools.  Production opens contexts with
@@ -163,6 +164,7 @@ typedef struct bgv_cfg {
   int32_t lines;        /* -1 auto; 0 / 1 fixed-argument lines (bulk mode, one-lane loop) */
   int32_t defer_pct;    /* -1 auto; 0..100: share of the G2 subgroup checks run beside the Miller loops (bulk mode) */
   int32_t timing;       /* -1 auto (batches >= 65,536 sets); 0 / 1 per-stage timing events */
+  int32_t clear_lanes;  /* -1 auto; 3 / 9 lanes per point of the latency mode's cofactor clearing */
 } bgv_cfg;
 /* every field "auto" */
 void bgv_cfg_default(bgv_cfg* cfg);

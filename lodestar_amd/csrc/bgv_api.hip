@@ -159,7 +159,7 @@ void bgv_cfg_default(bgv_cfg* cfg) {
   if (!cfg) return;
   memset(cfg, 0, sizeof *cfg);
   cfg->struct_size = sizeof *cfg;
-  cfg->split = cfg->miller = cfg->msm = cfg->prefold = cfg->lines = cfg->defer_pct = cfg->timing = -1;
+  cfg->split = cfg->miller = cfg->msm = cfg->prefold = cfg->lines = cfg->defer_pct = cfg->timing = cfg->clear_lanes = -1;
   cfg->job_lanes = cfg->pairs = 0;
 }
 
@@ -178,6 +178,8 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
     if (k.job_lanes != 0 && !lanes_ok(k.job_lanes)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.job_lanes %d", k.job_lanes);
     if (k.pairs < 0 || k.pairs > 2) return fail(BGV_E_INVALID_ARG, "bgv_cfg.pairs %d", k.pairs);
     if (k.msm < -1 || k.msm > 2) return fail(BGV_E_INVALID_ARG, "bgv_cfg.msm %d", k.msm);
+    if (k.clear_lanes != -1 && k.clear_lanes != 3 && k.clear_lanes != 9)
+      return fail(BGV_E_INVALID_ARG, "bgv_cfg.clear_lanes %d", k.clear_lanes);
     if (k.defer_pct < -1 || k.defer_pct > 100) return fail(BGV_E_INVALID_ARG, "bgv_cfg.defer_pct %d", k.defer_pct);
   }
   int n = 0;
@@ -474,10 +476,11 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   //    (25,088 sets: 24.5 ms split against 26.3 ms; 50,176: 35.4 against 29.3);
   //  * two pairs per Miller work item only when the batch alone fills the chip.
   static const uint32_t MILLER18_MIN = 2000, MILLER6_MIN = 6000, MILLER1_MIN = 35000, MSM_MIN = 6000, SPLIT_MAX = 35000,
-                        PAIRS2_MIN = 65536;
+                        PAIRS2_MIN = 65536, CLEAR3_MIN = 6000;
   const bgv_cfg& k = c->cfg;
   d.pairs_per_item = k.pairs ? (uint32_t)k.pairs : (n >= PAIRS2_MIN ? 2u : 1u);
   d.split = k.split >= 0 ? (uint32_t)k.split : (n < SPLIT_MAX ? 1u : 0u);
+  d.clear_lanes = k.clear_lanes > 0 ? (uint32_t)k.clear_lanes : (n < CLEAR3_MIN ? 9u : 3u);
   // sum r_i sigma_i per job by a bucket MSM (16 x 4-bit windows) when jobs
   // are block-sized (<= 256 sets).  The latency mode takes the fused kernel
   // (one workgroup per job, k_msm_fused: short chain, many idle lanes); bulk
@@ -676,6 +679,7 @@ static void stats_layout(bgv_stats* s, const dev_batch& d) {
   s->msm = d.msm;
   s->lines = d.lines;
   s->defer_from = d.defer_grp ? d.defer_from : d.n_sets;
+  s->clear_lanes = d.clear_lanes;
 }
 
 // job results, set codes and the batch flag through pinned memory; the

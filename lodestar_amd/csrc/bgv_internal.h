@@ -24,6 +24,7 @@ struct dev_batch {
   uint32_t pairs_per_item;  // Miller pairs sharing one accumulator (1, or 2 for batches that fill the GPU)
   uint32_t msm;             // 1: per-job bucket MSM for sum r_i sigma_i (k_msm_*), 0: per-set [r_i] sigma_i + tree
   uint32_t split;           // 1: latency mode: hash maps on two lanes per set, subgroup check beside [r_i] sigma_i
+  uint32_t clear_lanes;     // latency mode: lanes per point of the cofactor clearing (9, or 3)
   uint32_t prefold_log2;    // >0: two-level job fold, groups of 2^prefold_log2 sets (k_job_prefold); 0: one level
   uint32_t lines;           // one-lane Miller loop over fixed-argument lines: the hash stream stores every set's
                             // 68 unevaluated lines (launch_lines), k_miller evaluates them at P (pairing.h)
@@ -128,6 +129,7 @@ void launch_sig_check(hipStream_t st, const dev_batch& b, const dev_work& w);   
 void launch_sig_fixup(hipStream_t st, const dev_batch& b, const dev_work& w);   // k_sig_fix + k_job_recode
 void launch_sig_split_coop(hipStream_t st, const dev_batch& b, const dev_work& w);   // bgv_latency.hip
 void launch_hash_clear_coop(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_latency.hip
+void launch_hash_clear_trio(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_latency.hip
 void launch_fp12_tail(hipStream_t st, int stage, const dev_batch& b, const dev_work& w);  // bgv_tail.hip
 void launch_combine_final(hipStream_t st, const fp12_t* parts, uint32_t n, uint32_t* flag);
 void launch_final_exp_many(hipStream_t st, const fp12_t* in, fp12_t* out, uint32_t n);  // bgv_debug_stages

@@ -1105,7 +1105,9 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
     case ST_HASH:
       if (b.split) {
         BGV_LAUNCH(k_hash_map, 2u * b.n_sets, b, w);
-        if (BGV_COOP_G2) {
+        if (b.clear_lanes == 3) {
+          launch_hash_clear_trio(st, b, w);  // bgv_latency.hip
+        } else if (BGV_COOP_G2) {
           launch_hash_clear_coop(st, b, w);  // bgv_latency.hip
         } else {
           BGV_LAUNCH(k_hash_clear, b.n_sets, b, w);

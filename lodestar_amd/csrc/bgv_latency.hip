@@ -44,11 +44,11 @@ __global__ void __launch_bounds__(64, 1) k_sig_split_coop(dev_batch b, dev_work 
   g2j p;
   jac_from_aff(p, w.sig_aff[i]);
   if (check) {
-    const bool ok = !live || cg_in_subgroup(&sm[grp], s, q, p);
+    const bool ok = !live || cg_in_subgroup<3>(&sm[grp], s, q, p);
     if (lead) w.sig_grp[i] = ok ? 1u : 0u;
   } else {
     g2j r;
-    if (live) cg_mul_u64_w4(&sm[grp], tabs[grp], s, q, r, p, b.scalars[i]);
+    if (live) cg_mul_u64_w4<3>(&sm[grp], tabs[grp], s, q, r, p, b.scalars[i]);
     else jac_set_inf(r);  // infinity signature: blst skips it (adds the identity)
     if (lead) w.rsig[i] = r;
   }
@@ -61,13 +61,38 @@ __global__ void __launch_bounds__(64, 1) k_hash_clear_coop(dev_batch b, dev_work
   const bool own = grp < CG_GROUPS && i0 < b.n_sets;
   const uint32_t i = own ? i0 : 0u;
   g2j r, h;
-  cg_add(&sm[grp], s, q, r, w.q_part[2u * i], w.q_part[2u * i + 1u]);
-  cg_clear_cofactor(&sm[grp], s, q, h, r);
+  cg_add<3>(&sm[grp], s, q, r, w.q_part[2u * i], w.q_part[2u * i + 1u]);
+  cg_clear_cofactor<3>(&sm[grp], s, q, h, r);
   if (own && s == 0 && q == 0) {
     g2a ha;
     jac_to_aff(ha, h);
     w.h_aff[i] = ha;
   }
+}
+
+// The cofactor clearing on THREE lanes per point (coop_g2.h with one slot:
+// the sub-lanes of one Fp2 product, products in turn), 21 points per wave:
+// half the SIMD-time of the nine-lane layout for mid-size batches, where
+// nine lanes per point oversubscribe the chip (12,544 sets: 1,792 waves)
+constexpr int CG3_GROUPS = 21;
+__global__ void __launch_bounds__(64, 1) k_hash_clear_trio(dev_batch b, dev_work w) {
+  __shared__ cg_scratch sm[CG3_GROUPS + 1];
+  const uint32_t lane = threadIdx.x, grp = lane / 3u, q = lane % 3u;
+  const uint32_t i0 = blockIdx.x * CG3_GROUPS + grp;
+  const bool own = grp < (uint32_t)CG3_GROUPS && i0 < b.n_sets;
+  const uint32_t i = own ? i0 : 0u;
+  g2j r, h;
+  cg_add<1>(&sm[grp], 0u, q, r, w.q_part[2u * i], w.q_part[2u * i + 1u]);
+  cg_clear_cofactor<1>(&sm[grp], 0u, q, h, r);
+  if (own && q == 0) {
+    g2a ha;
+    jac_to_aff(ha, h);
+    w.h_aff[i] = ha;
+  }
+}
+
+void launch_hash_clear_trio(hipStream_t st, const dev_batch& b, const dev_work& w) {
+  if (b.n_sets) hipLaunchKernelGGL(k_hash_clear_trio, dim3((b.n_sets + CG3_GROUPS - 1) / CG3_GROUPS), dim3(64), 0, st, b, w);
 }
 
 void launch_sig_split_coop(hipStream_t st, const dev_batch& b, const dev_work& w) {

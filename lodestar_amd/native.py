@@ -93,8 +93,9 @@ class BgvStats(ctypes.Structure):
         ("msm", ctypes.c_uint32),
         ("lines", ctypes.c_uint32),
         ("defer_from", ctypes.c_uint32),
+        ("clear_lanes", ctypes.c_uint32),
     ]
-    LAYOUT = ("split", "miller_lanes", "pairs_per_item", "msm", "lines", "defer_from")
+    LAYOUT = ("split", "miller_lanes", "pairs_per_item", "msm", "lines", "defer_from", "clear_lanes")
 
     def as_dict(self, lib=None):
         names = [lib.stage_name(i) for i in range(N_STAGES)] if lib else [str(i) for i in range(N_STAGES)]
@@ -119,9 +120,9 @@ class BgvCfg(ctypes.Structure):
     Production contexts use the defaults (every field "auto")."""
     _fields_ = [("struct_size", ctypes.c_uint32)] + [
         (k, ctypes.c_int32) for k in
-        ("split", "miller", "job_lanes", "msm", "pairs", "prefold", "lines", "defer_pct", "timing")]
+        ("split", "miller", "job_lanes", "msm", "pairs", "prefold", "lines", "defer_pct", "timing", "clear_lanes")]
     AUTO = {"split": -1, "miller": -1, "job_lanes": 0, "msm": -1, "pairs": 0, "prefold": -1, "lines": -1,
-            "defer_pct": -1, "timing": -1}
+            "defer_pct": -1, "timing": -1, "clear_lanes": -1}
 
     @classmethod
     def make(cls, **over) -> "BgvCfg":

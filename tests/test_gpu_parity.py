@@ -375,8 +375,8 @@ def test_latency_split_mode_bit_identical():
     off-curve and out-of-subgroup signatures)."""
     from lodestar_amd import native
     outs = {}
-    for mode in ("0", "1"):
-        d = native.Device(0, split=int(mode))
+    for mode in ("0", "1", "1c3"):
+        d = native.Device(0, split=int(mode[0]), **({"clear_lanes": 3} if mode == "1c3" else {}))
         try:
             G.load_golden_table(d)
             a, expected, codes = G.golden_arrays([0, 1, 9, 11, 12, 13], scalars_seed=3)
@@ -390,8 +390,8 @@ def test_latency_split_mode_bit_identical():
             outs[mode] = (part, ok, jr.tolist(), sc.tolist(), jr2.tolist(), bad)
         finally:
             d.close()
-    assert outs["0"][0] == outs["1"][0]
-    assert outs["0"][1:5] == outs["1"][1:5]
+    assert outs["0"][0] == outs["1"][0] == outs["1c3"][0]
+    assert outs["0"][1:5] == outs["1"][1:5] == outs["1c3"][1:5]
     assert outs["1"][2] == gexp and outs["1"][3] == gcodes
     assert outs["1"][4] == np.where(outs["1"][5], 0, 1).tolist()
 

@@ -27,7 +27,7 @@ pytestmark = pytest.mark.gpu
 MODES = {
     "latency": {},
     "coop6_jobs18": {"miller": 6, "job_lanes": 18},
-    "duo_msm_fused": {"miller": 2, "msm": 1},
+    "duo_msm_fused_clear3": {"miller": 2, "msm": 1, "clear_lanes": 3},
     "bulk": {"split": 0},
     "bulk_serial_msm": {"split": 0, "miller": 1, "msm": 1, "pairs": 1},
     "c4_path": {"split": 0, "miller": 1, "msm": 1, "pairs": 2},

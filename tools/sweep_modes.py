@@ -28,6 +28,9 @@ MODES = {  # bgv_cfg overrides (include/bgv.h)
     "split1_serial": {"split": 1, "miller": 1, "msm": 0},
     "split1_coop_msm": {"split": 1, "miller": 36, "msm": 1},
     "m2": {"miller": 2},
+    "c3": {"clear_lanes": 3},
+    "c9": {"clear_lanes": 9},
+    "m2c3": {"miller": 2, "clear_lanes": 3},
     "m6": {"miller": 6},
     "m18": {"miller": 18},
     "m36": {"miller": 36},
