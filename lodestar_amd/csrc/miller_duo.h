@@ -133,14 +133,14 @@ __device__ __forceinline__ void duo_line(fp6_t& fh, const fp2_t& a0, const fp2_t
   fp6_t f0, f1, s, a, r;
   duo_halves(f0, f1, fh, h, X);
   fp6_add(s, f0, f1);
-  duo_sel6(a, hi, f0, s);
+  duo_sel6(a, hi, s, f0);
   fp2_t c, ab;
   fp2_add(ab, a1, b1);
-  c = duo_sel2(hi, a1, ab);
+  c = duo_sel2(hi, ab, a1);
   fp6_mul_01(r, a, a0, c);  // lane 0 P1 = f0 (a0, a1, 0) | lane 1 P3 = (f0 + f1)(a0, a1 + b1, 0)
   fp2_t u, vv;
   {
-    const fp2_t p = duo_sel2(hi, f1.c2, f1.c1);
+    const fp2_t p = duo_sel2(hi, f1.c1, f1.c2);
     fp2_mul(u, p, b1);        // lane 0 f1.c2 b1 (P2.c0 / xi) | lane 1 f1.c1 b1 (P2.c2)
     fp2_mul(vv, f1.c0, b1);   // both P2.c1
   }
@@ -159,7 +159,7 @@ __device__ __forceinline__ void duo_line(fp6_t& fh, const fp2_t& a0, const fp2_t
   fp6_add(o0, p1, vp2);
   fp6_sub(o1, p3, p1);
   fp6_sub(o1, o1, p2);
-  duo_sel6(fh, hi, o0, o1);
+  duo_sel6(fh, hi, o1, o0);
 }
 
 // the pair (P, Q) on lanes (2k, 2k+1): fh = this lane's half of f_{x,Q}(P)

@@ -22,7 +22,7 @@ sys.path.insert(0, ROOT)
 CALLS = os.path.join(ROOT, "gpurun_out", "size_trace_calls.json")
 
 
-def run(sizes, reps):
+def run(sizes, reps, cfg):
     import numpy as np
     import torch
 
@@ -32,7 +32,7 @@ def run(sizes, reps):
 
     dev = torch.device("cuda", 0)
     seg = bench.build_segment(list(range(max(sizes) // bench.SETS_PER_BLOCK)))
-    d = native.Device(0)
+    d = native.Device(0, **cfg)
     d.gen_keys(0, bench.N_VALIDATORS, bench.SEED)
     calls = []
     for n in sizes:
@@ -81,13 +81,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", default="3136,12544")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--cfg", default="{}", help="bgv_cfg overrides as JSON, e.g. '{\"miller\": 2}'")
     ap.add_argument("--analyze")
     ap.add_argument("--calls", default=CALLS)
     a = ap.parse_args()
     if a.analyze:
         analyze(a.analyze, a.calls)
     else:
-        run([int(x) for x in a.sizes.split(",")], a.reps)
+        run([int(x) for x in a.sizes.split(",")], a.reps, json.loads(a.cfg))
 
 
 if __name__ == "__main__":

@@ -31,6 +31,13 @@ MODES = {  # bgv_cfg overrides (include/bgv.h)
     "c3": {"clear_lanes": 3},
     "c9": {"clear_lanes": 9},
     "m2c3": {"miller": 2, "clear_lanes": 3},
+    "m2c9": {"miller": 2, "clear_lanes": 9},
+    "msm0c3": {"msm": 0, "clear_lanes": 3},
+    "msm0c9": {"msm": 0, "clear_lanes": 9},
+    "msm0m2c3": {"msm": 0, "miller": 2, "clear_lanes": 3},
+    "msm0m2c9": {"msm": 0, "miller": 2, "clear_lanes": 9},
+    "msm2c3": {"msm": 2, "clear_lanes": 3},
+    "msm2m2c3": {"msm": 2, "miller": 2, "clear_lanes": 3},
     "m6": {"miller": 6},
     "m18": {"miller": 18},
     "m36": {"miller": 36},
