@@ -144,7 +144,7 @@ typedef struct bgv_stats {
   uint32_t split;               /* 1: latency-mode hash and signature kernels */
   uint32_t miller_lanes;        /* set-pair Miller loop: lanes per pair (1 = one-lane loop) */
   uint32_t pairs_per_item;      /* one-lane loop: pairs sharing an accumulator */
-  uint32_t msm;                 /* 1: per-job bucket MSM for sum r_i sigma_i */
+  uint32_t msm;                 /* sum r_i sigma_i variant (bgv_cfg.msm) */
   uint32_t lines;               /* 1: fixed-argument Miller lines */
   uint32_t defer_from;          /* subgroup checks of sets >= defer_from run beside the Miller loops (n_sets: none) */
   uint32_t clear_lanes;         /* latency mode: lanes per point of the cofactor clearing */
@@ -156,9 +156,10 @@ typedef struct bgv_stats {
 typedef struct bgv_cfg {
   uint32_t struct_size; /* sizeof(bgv_cfg) */
   int32_t split;        /* -1 auto; 0 bulk kernels; 1 latency mode (two-lane hash maps, cooperative G2) */
-  int32_t miller;       /* -1 auto; 1 one-lane set-pair loop; 2 two-lane loop; 6 / 18 / 36 lanes per pair (cooperative) */
+  int32_t miller;       /* -1 auto; 1 one-lane set-pair loop; 2 / 4 two- / four-lane loop; 6 / 18 / 36 lanes per pair (cooperative) */
   int32_t job_lanes;    /* 0 auto (36); 6 / 18 / 36: lanes of the per-job (-G1, S_job) pairs */
-  int32_t msm;          /* -1 auto; 0 per-set [r_i] sigma_i + tree; 1 per-job bucket MSM (one workgroup per job); 2 the (job, window)-lane MSM (A/B) */
+  int32_t msm;          /* -1 auto; 0 per-set [r_i] sigma_i + tree; 1 per-job bucket MSM (one workgroup per job); 2 the (job, window)-lane MSM;
+                           3 one-lane per-set [r_i] sigma_i + tree, subgroup checks deferred */
   int32_t pairs;        /* 0 auto; 1 / 2 pairs per one-lane Miller work item */
   int32_t prefold;      /* -1 auto; 0 / 1 two-level per-job Miller fold */
   int32_t lines;        /* -1 auto; 0 / 1 fixed-argument lines (bulk mode, one-lane loop) */

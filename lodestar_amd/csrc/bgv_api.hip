@@ -174,10 +174,10 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
     if (cfg->struct_size != sizeof k) return fail(BGV_E_INVALID_ARG, "bgv_cfg.struct_size %u, expected %zu", cfg->struct_size, sizeof k);
     k = *cfg;
     auto lanes_ok = [](int v) { return v == 6 || v == 18 || v == 36; };
-    if (k.miller != -1 && k.miller != 1 && k.miller != 2 && !lanes_ok(k.miller)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.miller %d", k.miller);
+    if (k.miller != -1 && k.miller != 1 && k.miller != 2 && k.miller != 4 && !lanes_ok(k.miller)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.miller %d", k.miller);
     if (k.job_lanes != 0 && !lanes_ok(k.job_lanes)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.job_lanes %d", k.job_lanes);
     if (k.pairs < 0 || k.pairs > 2) return fail(BGV_E_INVALID_ARG, "bgv_cfg.pairs %d", k.pairs);
-    if (k.msm < -1 || k.msm > 2) return fail(BGV_E_INVALID_ARG, "bgv_cfg.msm %d", k.msm);
+    if (k.msm < -1 || k.msm > 3) return fail(BGV_E_INVALID_ARG, "bgv_cfg.msm %d", k.msm);
     if (k.clear_lanes != -1 && k.clear_lanes != 3 && k.clear_lanes != 9)
       return fail(BGV_E_INVALID_ARG, "bgv_cfg.clear_lanes %d", k.clear_lanes);
     if (k.defer_pct < -1 || k.defer_pct > 100) return fail(BGV_E_INVALID_ARG, "bgv_cfg.defer_pct %d", k.defer_pct);
@@ -475,8 +475,15 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   //  * latency mode (two-lane hash maps, cooperative G2) below SPLIT_MAX
   //    (25,088 sets: 24.5 ms split against 26.3 ms; 50,176: 35.4 against 29.3);
   //  * two pairs per Miller work item only when the batch alone fills the chip.
-  static const uint32_t MILLER18_MIN = 2000, MILLER6_MIN = 6000, MILLER1_MIN = 35000, MSM_MIN = 6000, SPLIT_MAX = 35000,
-                        PAIRS2_MIN = 65536, CLEAR3_MIN = 6000;
+  //  * r03 mid-size sweep (profiles/r03_sweep_mid_sizes.jsonl): the
+  //    four-lane Miller loop from 6,000 sets and the two-lane one from
+  //    18,000; the three-lane cofactor clearing from 9,000; sum r_i sigma_i
+  //    by one-lane per-set scaling with the subgroup checks deferred from
+  //    9,000 and by the (job, window) MSM from 18,000
+  //    (12,544: 18.4 -> 11.0 ms; 25,088: 24.1 -> 16.8 ms; 6,272: 10.8 -> 9.2 ms)
+  static const uint32_t MILLER18_MIN = 2000, MILLER4_MIN = 6000, MILLER2_MIN = 18000, MILLER1_MIN = 35000,
+                        MSM_MIN = 6000, MSM3_MIN = 9000, MSM2_MIN = 18000, SPLIT_MAX = 35000, PAIRS2_MIN = 65536,
+                        CLEAR3_MIN = 9000;
   const bgv_cfg& k = c->cfg;
   d.pairs_per_item = k.pairs ? (uint32_t)k.pairs : (n >= PAIRS2_MIN ? 2u : 1u);
   d.split = k.split >= 0 ? (uint32_t)k.split : (n < SPLIT_MAX ? 1u : 0u);
@@ -487,7 +494,14 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   // batches the (job, window)-lane kernels, which do a third of its SIMD-time
   // (C4: k_msm_fused 49 ms beside the hash, pubkeys and Miller loops,
   // stretching the Miller kernel from 14.5 to 26.4 ms, r03 trace)
-  d.msm = k.msm >= 0 ? (uint32_t)k.msm : ((n >= MSM_MIN && d.span_log2 <= 8) ? (d.split ? 1u : 2u) : 0u);
+  {
+    uint32_t auto_msm = 0;
+    if (n >= MSM_MIN && d.span_log2 <= 8) {
+      if (!d.split || n >= MSM2_MIN) auto_msm = 2;
+      else auto_msm = n < MSM3_MIN ? 1 : 3;
+    }
+    d.msm = k.msm >= 0 ? (uint32_t)k.msm : auto_msm;
+  }
   // Deferred subgroup checks: the signature stage only decodes, and the checks
   // of sets [defer_from, n) run beside the Miller loops (bgv_kernels.hip
   // k_job_recode).  Wherever the MSM sums the signatures (the latency mode
@@ -513,7 +527,8 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   // waves stay near one per SIMD (a pair's loop is a chain of ~1,800 Fp2
   // products on 6 lanes, ~560 product rounds on 36)
   d.miller_coop = k.miller >= 0 ? (k.miller == 1 ? 0u : (uint32_t)k.miller)
-                                : (n < MILLER18_MIN ? 36u : n < MILLER6_MIN ? 18u : n < MILLER1_MIN ? 6u : 0u);
+                                : (n < MILLER18_MIN ? 36u : n < MILLER4_MIN ? 18u : n < MILLER2_MIN ? 4u
+                                   : n < MILLER1_MIN ? 2u : 0u);
   // fixed-argument lines (pairing.h miller_lines): the G2 half of the one-lane
   // Miller loop moves to the hash stream, phase 1 (C4 40.4 -> 39.5 ms); with
   // one pair per item it loses (C4/2 26.4 -> 28.5 ms)

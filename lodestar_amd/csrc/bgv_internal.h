@@ -18,11 +18,13 @@ struct dev_batch {
   uint32_t n_sets, n_jobs, n_raw, table_n;
   uint32_t span_log2;    // per-job reduction tree covers 2^span_log2 sets
   uint32_t chunk_bound;  // upper bound of pubkey chunks (grid of k_pk_chunk)
-  uint32_t miller_coop;     // set pairs: 0 one-lane Miller loop (k_miller), 2 the two-lane loop
-                            // (k_miller_duo), else lanes per pair of the cooperative loop (miller_coop.h: 6, 18 or 36)
+  uint32_t miller_coop;     // set pairs: 0 one-lane Miller loop (k_miller), 2 / 4 the two- / four-lane loop
+                            // (k_miller_duo / k_miller_quad), else lanes per pair of the cooperative loop (miller_coop.h: 6, 18 or 36)
   uint32_t job_lanes;       // (-G1, S_job) pairs: lanes per pair of the cooperative loop (6, 18 or 36)
   uint32_t pairs_per_item;  // Miller pairs sharing one accumulator (1, or 2 for batches that fill the GPU)
-  uint32_t msm;             // 1: per-job bucket MSM for sum r_i sigma_i (k_msm_*), 0: per-set [r_i] sigma_i + tree
+  uint32_t msm;             // sum r_i sigma_i: 0 per-set [r_i] sigma_i + tree (latency mode: cooperative, with the checks),
+                            // 1 per-job fused MSM (k_msm_fused), 2 (job, window)-lane MSM (k_msm_*), 3 one-lane per-set
+                            // scaling + tree with the subgroup checks deferred (latency-mode hash)
   uint32_t split;           // 1: latency mode: hash maps on two lanes per set, subgroup check beside [r_i] sigma_i
   uint32_t clear_lanes;     // latency mode: lanes per point of the cofactor clearing (9, or 3)
   uint32_t prefold_log2;    // >0: two-level job fold, groups of 2^prefold_log2 sets (k_job_prefold); 0: one level
@@ -125,6 +127,7 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
 void launch_miller(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_miller.hip
 void launch_lines(hipStream_t st, const dev_batch& b, const dev_work& w);   // bgv_miller.hip
 void launch_miller_duo(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_miller.hip
+void launch_miller_quad(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_miller.hip
 void launch_sig_check(hipStream_t st, const dev_batch& b, const dev_work& w);   // subgroup checks only (sig_grp)
 void launch_sig_fixup(hipStream_t st, const dev_batch& b, const dev_work& w);   // k_sig_fix + k_job_recode
 void launch_sig_split_coop(hipStream_t st, const dev_batch& b, const dev_work& w);   // bgv_latency.hip

@@ -1126,7 +1126,7 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       if (b.split && !b.msm) break;  // [r_i] sigma_i already ran in k_sig_split
       if (b.msm == 2) {
         BGV_LAUNCH(k_msm_bucket, b.n_jobs * 16u, b, w);
-      } else if (b.msm) {
+      } else if (b.msm == 1) {
         if (b.n_jobs) {
           const uint32_t chunk = 1u << min(b.span_log2, 8u);  // LDS for one chunk of signatures
           hipLaunchKernelGGL(k_msm_fused, dim3(b.n_jobs), dim3(MSM_LANES), chunk * sizeof(g2a), st, b, w, chunk);
@@ -1142,7 +1142,7 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
         BGV_LAUNCH(k_msm_job, b.n_jobs, b, w);
         break;
       }
-      if (b.msm) {
+      if (b.msm == 1) {
         BGV_LAUNCH(k_job_code, b.n_jobs, b, w);
         break;
       }
@@ -1152,6 +1152,10 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
     case ST_MILLER:  // (r_i PK_i, H(m_i)) pairs: needs ST_HASH and ST_PK only
       if (b.miller_coop == 2) {
         launch_miller_duo(st, b, w);  // bgv_miller.hip
+        break;
+      }
+      if (b.miller_coop == 4) {
+        launch_miller_quad(st, b, w);  // bgv_miller.hip
         break;
       }
       if (b.miller_coop) {

@@ -36,6 +36,7 @@
 #endif
 #include "bgv_internal.h"
 #include "miller_duo.h"
+#include "miller_quad.h"
 
 namespace bgv {
 
@@ -108,6 +109,39 @@ __global__ void __launch_bounds__(64, 1) k_miller_duo(dev_batch b, dev_work w, u
 
 void launch_miller_duo(hipStream_t st, const dev_batch& b, const dev_work& w) {
   if (b.n_sets) hipLaunchKernelGGL(k_miller_duo, dim3((b.n_sets + 31u) / 32u), dim3(64), 0, st, b, w, b.n_sets);
+}
+
+// Four lanes per pair (miller_quad.h), 16 pairs per wave: the layout for
+// batches of ~6,000 to ~25,000 sets (prepare()), where two lanes per pair
+// leave most SIMDs idle and the cooperative six-lane layout oversubscribes
+// them at three times the per-iteration work.
+__global__ void __launch_bounds__(64, 1) k_miller_quad(dev_batch b, dev_work w, uint32_t count) {
+  __shared__ quad_x_t sx[16];
+  const uint32_t lane = threadIdx.x, pr = lane >> 2, h = (lane >> 1) & 1u, s = lane & 1u;
+  const uint32_t t = blockIdx.x * 16u + pr;
+  if (t >= count) return;  // the four lanes of a pair leave together
+  if (w.pk_code[t] != C_OK) {  // rejected job: its Miller values are never used
+    if (s == 0) {
+      fp6_t v;
+      if (h) fp6_zero(v);
+      else fp6_one(v);
+      if (h) w.f_set[t].c1 = v;
+      else w.f_set[t].c0 = v;
+    }
+    return;
+  }
+  const g1a P = w.rpk_aff[t];
+  const g2a Q = w.h_aff[t];
+  fp6_t fh;
+  quad_miller(fh, P, Q, h, s, sx[pr]);
+  if (s == 0) {
+    if (h) w.f_set[t].c1 = fh;
+    else w.f_set[t].c0 = fh;
+  }
+}
+
+void launch_miller_quad(hipStream_t st, const dev_batch& b, const dev_work& w) {
+  if (b.n_sets) hipLaunchKernelGGL(k_miller_quad, dim3((b.n_sets + 15u) / 16u), dim3(64), 0, st, b, w, b.n_sets);
 }
 
 // the unevaluated lines of every set's H(m) (pairing.h miller_lines), on the

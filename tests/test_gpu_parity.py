@@ -221,13 +221,14 @@ def test_microbench_runs(dev):
 
 def test_cooperative_miller_bit_identical_to_serial():
     """The cooperative Miller loop (miller_coop.h) in its three layouts (36,
-    6 and 18 lanes per pair), the two-lane loop (miller_duo.h) and the
+    6 and 18 lanes per pair), the two- and four-lane loops (miller_duo.h,
+    miller_quad.h) and the
     one-lane loop (pairing.h, bgv_cfg.miller = 1)
     produce the same Fp12 batch partial, byte for byte, and the same verdicts."""
     from lodestar_amd import native
     outs = {}
-    for mode in ("serial", "coop", "6", "18", "duo"):
-        d = native.Device(0, miller={"serial": 1, "coop": 36, "6": 6, "18": 18, "duo": 2}[mode])
+    for mode in ("serial", "coop", "6", "18", "duo", "quad"):
+        d = native.Device(0, miller={"serial": 1, "coop": 36, "6": 6, "18": 18, "duo": 2, "quad": 4}[mode])
         try:
             G.load_golden_table(d)
             a, expected, _ = G.golden_arrays([0, 1, 9, 11, 12, 13], scalars_seed=3)
@@ -240,7 +241,7 @@ def test_cooperative_miller_bit_identical_to_serial():
             outs[mode] = (part, ok, jr.tolist(), jr2.tolist(), bad)
         finally:
             d.close()
-    for mode in ("coop", "6", "18", "duo"):  # 36, 6, 18 and 2 lanes per pair
+    for mode in ("coop", "6", "18", "duo", "quad"):  # 36, 6, 18, 2 and 4 lanes per pair
         assert outs["serial"][0] == outs[mode][0], mode
         assert outs["serial"][1:4] == outs[mode][1:4], mode
     assert outs["coop"][2] == G.golden_arrays()[1]
@@ -343,8 +344,8 @@ def test_signature_msm_bit_identical_to_per_set_scaling():
     byte-identical, and the golden verdicts hold in both modes."""
     from lodestar_amd import native
     outs = {}
-    for mode in ("0", "1", "2"):
-        d = native.Device(0, msm=int(mode))
+    for mode in ("0", "1", "2", "3"):  # 3: one-lane scaling, checks deferred, in latency mode
+        d = native.Device(0, msm=int(mode), **({"split": 1} if mode == "3" else {}))
         try:
             G.load_golden_table(d)
             a, _, _ = G.golden_arrays([0, 1, 9, 10, 11, 12, 13], scalars_seed=5)
@@ -363,7 +364,7 @@ def test_signature_msm_bit_identical_to_per_set_scaling():
             outs[mode] = (part, ok, syn_part)
         finally:
             d.close()
-    assert outs["0"] == outs["1"] == outs["2"]
+    assert outs["0"] == outs["1"] == outs["2"] == outs["3"]
 
 
 @pytest.mark.gpu

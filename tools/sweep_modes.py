@@ -33,6 +33,16 @@ MODES = {  # bgv_cfg overrides (include/bgv.h)
     "m2c3": {"miller": 2, "clear_lanes": 3},
     "m2c9": {"miller": 2, "clear_lanes": 9},
     "msm0c3": {"msm": 0, "clear_lanes": 3},
+    "m4": {"miller": 4},
+    "m4msm3c3": {"miller": 4, "msm": 3, "clear_lanes": 3},
+    "m2msm3c3": {"miller": 2, "msm": 3, "clear_lanes": 3},
+    "m4msm3c9": {"miller": 4, "msm": 3, "clear_lanes": 9},
+    "m6msm3c9": {"miller": 6, "msm": 3, "clear_lanes": 9},
+    "m18msm3c9": {"miller": 18, "msm": 3, "clear_lanes": 9},
+    "m4msm0c3": {"miller": 4, "msm": 0, "clear_lanes": 3},
+    "m4msm2c3": {"miller": 4, "msm": 2, "clear_lanes": 3},
+    "m4msm1c9": {"miller": 4, "msm": 1, "clear_lanes": 9},
+    "m4msm0c9": {"miller": 4, "msm": 0, "clear_lanes": 9},
     "msm0c9": {"msm": 0, "clear_lanes": 9},
     "msm0m2c3": {"msm": 0, "miller": 2, "clear_lanes": 3},
     "msm0m2c9": {"msm": 0, "miller": 2, "clear_lanes": 9},
