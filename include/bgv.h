@@ -159,7 +159,7 @@ typedef struct bgv_cfg {
   int32_t miller;       /* -1 auto; 1 one-lane set-pair loop; 2 / 4 two- / four-lane loop; 6 / 18 / 36 lanes per pair (cooperative) */
   int32_t job_lanes;    /* 0 auto (36); 6 / 18 / 36: lanes of the per-job (-G1, S_job) pairs */
   int32_t msm;          /* -1 auto; 0 per-set [r_i] sigma_i + tree; 1 per-job bucket MSM (one workgroup per job); 2 the (job, window)-lane MSM;
-                           3 one-lane per-set [r_i] sigma_i + tree, subgroup checks deferred */
+                           3 one-lane per-set [r_i] sigma_i + tree, subgroup checks deferred; 4 the (job, window, digit)-lane MSM */
   int32_t pairs;        /* 0 auto; 1 / 2 pairs per one-lane Miller work item */
   int32_t prefold;      /* -1 auto; 0 / 1 two-level per-job Miller fold */
   int32_t lines;        /* -1 auto; 0 / 1 fixed-argument lines (bulk mode, one-lane loop) */

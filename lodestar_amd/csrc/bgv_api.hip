@@ -177,7 +177,7 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
     if (k.miller != -1 && k.miller != 1 && k.miller != 2 && k.miller != 4 && !lanes_ok(k.miller)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.miller %d", k.miller);
     if (k.job_lanes != 0 && !lanes_ok(k.job_lanes)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.job_lanes %d", k.job_lanes);
     if (k.pairs < 0 || k.pairs > 2) return fail(BGV_E_INVALID_ARG, "bgv_cfg.pairs %d", k.pairs);
-    if (k.msm < -1 || k.msm > 3) return fail(BGV_E_INVALID_ARG, "bgv_cfg.msm %d", k.msm);
+    if (k.msm < -1 || k.msm > 4) return fail(BGV_E_INVALID_ARG, "bgv_cfg.msm %d", k.msm);
     if (k.clear_lanes != -1 && k.clear_lanes != 3 && k.clear_lanes != 9)
       return fail(BGV_E_INVALID_ARG, "bgv_cfg.clear_lanes %d", k.clear_lanes);
     if (k.defer_pct < -1 || k.defer_pct > 100) return fail(BGV_E_INVALID_ARG, "bgv_cfg.defer_pct %d", k.defer_pct);
@@ -478,11 +478,11 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   //  * r03 mid-size sweep (profiles/r03_sweep_mid_sizes.jsonl): the
   //    four-lane Miller loop from 6,000 sets and the two-lane one from
   //    18,000; the three-lane cofactor clearing from 9,000; sum r_i sigma_i
-  //    by one-lane per-set scaling with the subgroup checks deferred from
-  //    9,000 and by the (job, window) MSM from 18,000
-  //    (12,544: 18.4 -> 11.0 ms; 25,088: 24.1 -> 16.8 ms; 6,272: 10.8 -> 9.2 ms)
+  //    by the (job, window, digit)-lane MSM from 9,000 (bulk batches: the
+  //    (job, window) one)
+  //    (12,544: 18.4 -> 10.6 ms; 25,088: 24.1 -> 16.9 ms; 6,272: 10.8 -> 9.2 ms)
   static const uint32_t MILLER18_MIN = 2000, MILLER4_MIN = 6000, MILLER2_MIN = 18000, MILLER1_MIN = 35000,
-                        MSM_MIN = 6000, MSM3_MIN = 9000, MSM2_MIN = 18000, SPLIT_MAX = 35000, PAIRS2_MIN = 65536,
+                        MSM_MIN = 6000, MSM4_MIN = 9000, SPLIT_MAX = 35000, PAIRS2_MIN = 65536,
                         CLEAR3_MIN = 9000;
   const bgv_cfg& k = c->cfg;
   d.pairs_per_item = k.pairs ? (uint32_t)k.pairs : (n >= PAIRS2_MIN ? 2u : 1u);
@@ -497,8 +497,8 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   {
     uint32_t auto_msm = 0;
     if (n >= MSM_MIN && d.span_log2 <= 8) {
-      if (!d.split || n >= MSM2_MIN) auto_msm = 2;
-      else auto_msm = n < MSM3_MIN ? 1 : 3;
+      if (!d.split) auto_msm = 2;
+      else auto_msm = n < MSM4_MIN ? 1 : 4;
     }
     d.msm = k.msm >= 0 ? (uint32_t)k.msm : auto_msm;
   }
@@ -601,6 +601,9 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
   if (d.msm == 2) {
     if ((r = c->msm_bucket.ensure(nj * 16 * 15)) || (r = c->msm_mask.ensure(nj * 16)) || (r = c->msm_win.ensure(nj * 16))) return r;
     w.msm_bucket = c->msm_bucket.p; w.msm_mask = c->msm_mask.p; w.msm_win = c->msm_win.p;
+  } else if (d.msm == 4) {
+    if ((r = c->msm_win.ensure(nj * 16))) return r;
+    w.msm_win = c->msm_win.p;
   }
   return 0;
 }

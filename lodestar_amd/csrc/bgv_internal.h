@@ -23,8 +23,9 @@ struct dev_batch {
   uint32_t job_lanes;       // (-G1, S_job) pairs: lanes per pair of the cooperative loop (6, 18 or 36)
   uint32_t pairs_per_item;  // Miller pairs sharing one accumulator (1, or 2 for batches that fill the GPU)
   uint32_t msm;             // sum r_i sigma_i: 0 per-set [r_i] sigma_i + tree (latency mode: cooperative, with the checks),
-                            // 1 per-job fused MSM (k_msm_fused), 2 (job, window)-lane MSM (k_msm_*), 3 one-lane per-set
-                            // scaling + tree with the subgroup checks deferred (latency-mode hash)
+                            // 1 per-job fused MSM (k_msm_fused), 2 (job, window)-lane MSM (k_msm_bucket), 3 one-lane per-set
+                            // scaling + tree with the subgroup checks deferred (latency-mode hash), 4 (job, window,
+                            // digit)-lane MSM (k_msm_digit)
   uint32_t split;           // 1: latency mode: hash maps on two lanes per set, subgroup check beside [r_i] sigma_i
   uint32_t clear_lanes;     // latency mode: lanes per point of the cofactor clearing (9, or 3)
   uint32_t prefold_log2;    // >0: two-level job fold, groups of 2^prefold_log2 sets (k_job_prefold); 0: one level
@@ -52,9 +53,9 @@ struct dev_work {
   g2a* h_aff;         // H(m)
   g2j* q_part;        // [2 n_sets] split mode: the two mapped points of every message
   uint32_t* sig_grp;  // split / defer_grp mode: signature passed the subgroup check
-  g2j* msm_bucket;    // [n_jobs * 16 windows * 15 buckets] (msm mode)
+  g2j* msm_bucket;    // [n_jobs * 16 windows * 15 buckets] (msm = 2)
   uint32_t* msm_mask; // [n_jobs * 16] occupied buckets of each (job, window)
-  g2j* msm_win;       // [n_jobs * 16] window sums
+  g2j* msm_win;       // [n_jobs * 16] window sums (msm = 2, 4)
   uint32_t* chunk_off;  // [n_sets + 1] scan of per-set pubkey chunk counts
   uint32_t* chunk_set;  // set of every chunk
   g1j* pk_part;         // per-chunk partial sums

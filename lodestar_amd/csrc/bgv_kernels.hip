@@ -474,7 +474,7 @@ __global__ void __launch_bounds__(64, BGV_SCALE_WAVES) k_sig_scale(dev_batch b, 
 // identity signatures add nothing: a job with a bad signature is rejected by
 // its code and never reaches the pairing.
 
-// lane = (job, window); the 15 buckets live in HBM/L2, `mask` marks the
+// msm = 2 (bulk batches): lane = (job, window); the 15 buckets live in HBM/L2, `mask` marks the
 // occupied ones (an unoccupied bucket is the identity: no initialisation)
 __global__ void BGV_BULK k_msm_bucket(dev_batch b, dev_work w) {
   const uint32_t t = gtid();
@@ -517,6 +517,69 @@ __global__ void BGV_BULK k_msm_window(dev_batch b, dev_work w) {
     jac_add(tot, tot, run);
   }
   w.msm_win[t] = tot;
+}
+
+// msm = 4 (mid-size batches, latency mode): lane = (job, window w, digit d),
+// 256 lanes per job (four windows per wave):
+//   1. bucket d of window w: the mixed sum of the job's signatures whose
+//      digit w is d, in registers (each lane walks the job's scalars to its
+//      next match; the wave runs as many additions as its fullest bucket);
+//   2. d B_d by MSB-first double-and-add (<= 3 doublings and additions);
+//   3. S_w = sum_d d B_d by a tree over the window's 16 lanes (cross-lane
+//      shuffles inside the wave, 4 levels); lane d = 0 writes S_w.
+// No bucket leaves the registers; the chain is ~max-bucket mixed additions +
+// 6 + 4 point operations (against the job's span + 30 of a (job, window)
+// lane walking all its sets and then its running sums).  Bulk batches keep
+// that form (msm = 2): a wave here runs its fullest bucket's additions, ~2x
+// the mean, which at C4 costs phase 1 ~1.2 ms (same-box A/B, r03).
+__device__ __forceinline__ void shfl_down16(g2j& r, const g2j& v, uint32_t st) {
+  const uint32_t* src = (const uint32_t*)&v;
+  uint32_t* dst = (uint32_t*)&r;
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(g2j) / 4); k++) dst[k] = (uint32_t)__shfl_down((int)src[k], st, 16);
+}
+
+__global__ void BGV_BULK k_msm_digit(dev_batch b, dev_work w) {
+  const uint32_t t = gtid();
+  const uint32_t j = t >> 8, win = (t >> 4) & 15u, d = t & 15u;
+  if (j >= b.n_jobs) return;  // whole waves: 256 lanes per job
+  const uint32_t beg = b.job_off[j], end = b.job_off[j + 1];
+  g2j acc;
+  jac_set_inf(acc);
+  bool first = true;
+  uint32_t i = beg;
+  for (;;) {
+    // this lane's next set whose digit in window `win` is d (digit 0 adds nothing)
+    while (i < end) {
+      const bool live = w.sig_code[i] == C_OK && !w.sig_inf[i];
+      const uint32_t dig = (uint32_t)(b.scalars[i] >> (4u * win)) & 15u;
+      if (live && d != 0 && dig == d) break;
+      i++;
+    }
+    if (!__any(i < end)) break;
+    if (i < end) {
+      const g2a s = w.sig_aff[i];
+      if (first) jac_from_aff(acc, s);
+      else jac_add_aff(acc, acc, s);
+      first = false;
+      i++;
+    }
+  }
+  // d B_d
+  const g2j base = acc;
+  for (int bit = 2; bit >= 0; bit--) {
+    if (d >> (bit + 1)) {
+      jac_dbl(acc, acc);
+      if ((d >> bit) & 1u) jac_add(acc, acc, base);
+    }
+  }
+  // S_w: lanes [st, 2 st) of the window hand their sums to lanes [0, st)
+  for (uint32_t st = 8; st >= 1; st >>= 1) {
+    g2j o;
+    shfl_down16(o, acc, st);
+    if (d < st) jac_add(acc, acc, o);
+  }
+  if (d == 0) w.msm_win[16u * j + win] = acc;
 }
 
 // per job: S_job = sum_w 16^w S_w (Horner), codes as k_job_s
@@ -1126,6 +1189,8 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       if (b.split && !b.msm) break;  // [r_i] sigma_i already ran in k_sig_split
       if (b.msm == 2) {
         BGV_LAUNCH(k_msm_bucket, b.n_jobs * 16u, b, w);
+      } else if (b.msm == 4) {
+        BGV_LAUNCH(k_msm_digit, b.n_jobs * 256u, b, w);
       } else if (b.msm == 1) {
         if (b.n_jobs) {
           const uint32_t chunk = 1u << min(b.span_log2, 8u);  // LDS for one chunk of signatures
@@ -1137,8 +1202,8 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       break;
     case ST_S_TREE:
       BGV_LAUNCH(k_set_job, b.n_jobs, b, w);
-      if (b.msm == 2) {
-        BGV_LAUNCH(k_msm_window, b.n_jobs * 16u, b, w);
+      if (b.msm == 2 || b.msm == 4) {
+        if (b.msm == 2) BGV_LAUNCH(k_msm_window, b.n_jobs * 16u, b, w);
         BGV_LAUNCH(k_msm_job, b.n_jobs, b, w);
         break;
       }

@@ -344,8 +344,8 @@ def test_signature_msm_bit_identical_to_per_set_scaling():
     byte-identical, and the golden verdicts hold in both modes."""
     from lodestar_amd import native
     outs = {}
-    for mode in ("0", "1", "2", "3"):  # 3: one-lane scaling, checks deferred, in latency mode
-        d = native.Device(0, msm=int(mode), **({"split": 1} if mode == "3" else {}))
+    for mode in ("0", "1", "2", "3", "4"):  # 3: one-lane scaling, checks deferred, in latency mode
+        d = native.Device(0, msm=int(mode), **({"split": 1} if mode in ("3", "4") else {}))
         try:
             G.load_golden_table(d)
             a, _, _ = G.golden_arrays([0, 1, 9, 10, 11, 12, 13], scalars_seed=5)
@@ -364,7 +364,7 @@ def test_signature_msm_bit_identical_to_per_set_scaling():
             outs[mode] = (part, ok, syn_part)
         finally:
             d.close()
-    assert outs["0"] == outs["1"] == outs["2"] == outs["3"]
+    assert outs["0"] == outs["1"] == outs["2"] == outs["3"] == outs["4"]
 
 
 @pytest.mark.gpu

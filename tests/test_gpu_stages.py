@@ -29,11 +29,12 @@ MODES = {
     "coop6_jobs18": {"miller": 6, "job_lanes": 18},
     "duo_msm_fused_clear3": {"miller": 2, "msm": 1, "clear_lanes": 3},
     "quad_msm0_clear3": {"miller": 4, "msm": 0, "clear_lanes": 3},
-    "quad_split_msm2": {"miller": 4, "msm": 2, "split": 1},
+    "quad_split_msm4": {"miller": 4, "msm": 4, "split": 1, "clear_lanes": 3},
     "quad_split_msm3": {"miller": 4, "msm": 3, "split": 1, "clear_lanes": 3},
     "bulk": {"split": 0},
     "bulk_serial_msm": {"split": 0, "miller": 1, "msm": 1, "pairs": 1},
-    "c4_path": {"split": 0, "miller": 1, "msm": 1, "pairs": 2},
+    "c4_path": {"split": 0, "miller": 1, "msm": 2, "pairs": 2},
+    "bulk_msm4": {"split": 0, "miller": 1, "msm": 4, "pairs": 1},
 }
 
 

@@ -41,6 +41,8 @@ MODES = {  # bgv_cfg overrides (include/bgv.h)
     "m18msm3c9": {"miller": 18, "msm": 3, "clear_lanes": 9},
     "m4msm0c3": {"miller": 4, "msm": 0, "clear_lanes": 3},
     "m4msm2c3": {"miller": 4, "msm": 2, "clear_lanes": 3},
+    "m4msm4c3": {"miller": 4, "msm": 4, "clear_lanes": 3},
+    "m2msm4c3": {"miller": 2, "msm": 4, "clear_lanes": 3},
     "m4msm1c9": {"miller": 4, "msm": 1, "clear_lanes": 9},
     "m4msm0c9": {"miller": 4, "msm": 0, "clear_lanes": 9},
     "msm0c9": {"msm": 0, "clear_lanes": 9},
