@@ -62,6 +62,7 @@ MODES = {  # bgv_cfg overrides (include/bgv.h)
     "msm1": {"msm": 1},
     "msm2": {"msm": 2},
     "nodefer": {"defer_pct": 0},
+    "d75": {"defer_pct": 75},
 }
 
 
