@@ -582,28 +582,36 @@ __global__ void BGV_BULK k_msm_digit(dev_batch b, dev_work w) {
   if (d == 0) w.msm_win[16u * j + win] = acc;
 }
 
-// per job: S_job = sum_w 16^w S_w (Horner), codes as k_job_s
+// per job: S_job = sum_w 16^w S_w, codes as k_job_s.  Lane (job, window w)
+// doubles its window sum 4 w times, then a tree over the job's 16 lanes
+// (cross-lane shuffles): 60 doublings + 4 additions on the chain instead of a
+// one-lane Horner's 60 doublings + 15 additions
 __global__ void BGV_BULK k_msm_job(dev_batch b, dev_work w) {
-  const uint32_t j = gtid();
-  if (j >= b.n_jobs) return;
+  const uint32_t t = gtid();
+  const uint32_t j = t >> 4, win = t & 15u;
+  if (j >= b.n_jobs) return;  // whole 16-lane groups (n_jobs * 16 lanes)
   const uint32_t beg = b.job_off[j], end = b.job_off[j + 1];
   int32_t code = C_OK;
   for (uint32_t i = beg; i < end && code == C_OK; i++) code = w.sig_code[i];
   for (uint32_t i = beg; i < end && code == C_OK; i++) code = w.pk_code[i];
   if (end == beg) code = C_EMPTY_JOB;
+  g2j s;
+  jac_set_inf(s);
+  if (code == C_OK) {
+    s = w.msm_win[16u * j + win];
+    for (uint32_t k = 0; k < 4u * win; k++) jac_dbl(s, s);
+  }
+  for (uint32_t st = 8; st >= 1; st >>= 1) {
+    g2j o;
+    shfl_down16(o, s, st);
+    if (win < st) jac_add(s, s, o);
+  }
+  if (win != 0) return;
   g2a sa;
   sa.x = fp2_zero();
   sa.y = fp2_zero();
   uint32_t inf = 1;
-  if (code == C_OK) {
-    g2j s = w.msm_win[16u * j + 15u];
-    for (int win = 14; win >= 0; win--) {
-      for (int k = 0; k < 4; k++) jac_dbl(s, s);
-      const g2j v = w.msm_win[16u * j + (uint32_t)win];
-      jac_add(s, s, v);
-    }
-    inf = jac_to_aff(sa, s) ? 0u : 1u;
-  }
+  if (code == C_OK) inf = jac_to_aff(sa, s) ? 0u : 1u;
   w.s_aff[j] = sa;
   w.s_inf[j] = inf;
   w.job_code[j] = code;
@@ -1204,7 +1212,7 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       BGV_LAUNCH(k_set_job, b.n_jobs, b, w);
       if (b.msm == 2 || b.msm == 4) {
         if (b.msm == 2) BGV_LAUNCH(k_msm_window, b.n_jobs * 16u, b, w);
-        BGV_LAUNCH(k_msm_job, b.n_jobs, b, w);
+        BGV_LAUNCH(k_msm_job, b.n_jobs * 16u, b, w);
         break;
       }
       if (b.msm == 1) {
