@@ -178,7 +178,7 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
     if (k.job_lanes != 0 && !lanes_ok(k.job_lanes)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.job_lanes %d", k.job_lanes);
     if (k.pairs < 0 || k.pairs > 2) return fail(BGV_E_INVALID_ARG, "bgv_cfg.pairs %d", k.pairs);
     if (k.msm < -1 || k.msm > 4) return fail(BGV_E_INVALID_ARG, "bgv_cfg.msm %d", k.msm);
-    if (k.clear_lanes != -1 && k.clear_lanes != 3 && k.clear_lanes != 9)
+    if (k.clear_lanes != -1 && k.clear_lanes != 1 && k.clear_lanes != 3 && k.clear_lanes != 9)
       return fail(BGV_E_INVALID_ARG, "bgv_cfg.clear_lanes %d", k.clear_lanes);
     if (k.defer_pct < -1 || k.defer_pct > 100) return fail(BGV_E_INVALID_ARG, "bgv_cfg.defer_pct %d", k.defer_pct);
   }
@@ -487,7 +487,9 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   const bgv_cfg& k = c->cfg;
   d.pairs_per_item = k.pairs ? (uint32_t)k.pairs : (n >= PAIRS2_MIN ? 2u : 1u);
   d.split = k.split >= 0 ? (uint32_t)k.split : (n < SPLIT_MAX ? 1u : 0u);
-  d.clear_lanes = k.clear_lanes > 0 ? (uint32_t)k.clear_lanes : (n < CLEAR3_MIN ? 9u : 3u);
+  // one lane per point from 18,000 sets (25,088: 16.74 -> 16.5 ms; the trio's
+  // 1,176 waves oversubscribe the SIMDs there)
+  d.clear_lanes = k.clear_lanes > 0 ? (uint32_t)k.clear_lanes : (n < CLEAR3_MIN ? 9u : n < MILLER2_MIN ? 3u : 1u);
   // sum r_i sigma_i per job by a bucket MSM (16 x 4-bit windows) when jobs
   // are block-sized (<= 256 sets).  The latency mode takes the fused kernel
   // (one workgroup per job, k_msm_fused: short chain, many idle lanes); bulk

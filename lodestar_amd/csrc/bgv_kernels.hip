@@ -1178,7 +1178,7 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
         BGV_LAUNCH(k_hash_map, 2u * b.n_sets, b, w);
         if (b.clear_lanes == 3) {
           launch_hash_clear_trio(st, b, w);  // bgv_latency.hip
-        } else if (BGV_COOP_G2) {
+        } else if (BGV_COOP_G2 && b.clear_lanes != 1) {
           launch_hash_clear_coop(st, b, w);  // bgv_latency.hip
         } else {
           BGV_LAUNCH(k_hash_clear, b.n_sets, b, w);

@@ -27,8 +27,15 @@
 #ifndef BGV_MILLER_LDS_F
 #define BGV_MILLER_LDS_F 1
 #endif
-// per-unit inlining knobs (A/B builds): Fp12 layer and Miller steps
-#ifdef BGV_MILLER_FP12_INLINE
+// per-unit inlining knobs (A/B builds): Fp12 layer and Miller steps.  The
+// Fp12 layer is inlined into the loops: a non-inlined fp12_sqr saved and
+// restored ~1.2 KB of callee-saved registers through scratch on every call
+// (k_miller: 11.2 GB FETCH + WRITE per C4 launch, profiles/r03_pmc_*.csv);
+// same-box A/B at C4: 39.04 / 38.82 -> 38.55 / 38.32 ms (r03)
+#ifndef BGV_MILLER_FP12_INLINE
+#define BGV_MILLER_FP12_INLINE 1
+#endif
+#if BGV_MILLER_FP12_INLINE
 #define BGV_FP12_INLINE BGV_MILLER_FP12_INLINE
 #endif
 #ifdef BGV_MILLER_STEP_INLINE

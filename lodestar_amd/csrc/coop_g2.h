@@ -68,16 +68,12 @@ BGV_CGF void cg_prod1(cg_scratch* S, uint32_t q, const fp2_t& a, const fp2_t& b,
   BGV_LDS cg_scratch* L = (BGV_LDS cg_scratch*)S;
   lds_put(&L->P[0][q], r);
   coop_wave_sync();
-  if (q < 2) {
-    const fp_t p0 = lds_get(&L->P[0][0]), p1 = lds_get(&L->P[0][1]);
-    fp_t w, c;
-    fp_add_sub(w, p0, p1, c, p0, p1);
-    if (q == 1) fp_sub(c, lds_get(&L->P[0][2]), w);
-    lds_put(&L->O[0][q], c);
-  }
-  coop_wave_sync();
-  o.c0 = lds_get(&L->O[0][0]);
-  o.c1 = lds_get(&L->O[0][1]);
+  // every lane combines (one dual add/sub and a subtraction: the same issue
+  // cost as two lanes combining, without a second exchange)
+  const fp_t p0 = lds_get(&L->P[0][0]), p1 = lds_get(&L->P[0][1]), p2 = lds_get(&L->P[0][2]);
+  fp_t w;
+  fp_add_sub(w, p0, p1, o.c0, p0, p1);
+  fp_sub(o.c1, p2, w);
   coop_wave_sync();
 }
 

@@ -30,6 +30,9 @@ MODES = {  # bgv_cfg overrides (include/bgv.h)
     "m2": {"miller": 2},
     "c3": {"clear_lanes": 3},
     "c9": {"clear_lanes": 9},
+    "c1": {"clear_lanes": 1},
+    "m4c1": {"miller": 4, "clear_lanes": 1},
+    "m2c1": {"miller": 2, "clear_lanes": 1},
     "m2c3": {"miller": 2, "clear_lanes": 3},
     "m2c9": {"miller": 2, "clear_lanes": 9},
     "msm0c3": {"msm": 0, "clear_lanes": 3},
