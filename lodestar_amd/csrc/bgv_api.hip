@@ -511,10 +511,11 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   // them with one pair per Miller item (C4/2 28.3 -> 26.4 ms); half with two
   // pairs per item: the Miller kernel leaves 240 SIMDs to the MSM tail and
   // the job pairs, and half of the checks fill them without outlasting it
-  // (C4, 3 runs each: none 39.75, 50% 39.27, 65% 39.31, all 39.89 ms).
+  // (C4, 3 runs each: none 39.75, 50% 39.27, 65% 39.31, all 39.89 ms; r03, with
+  // the inlined Fp12 layer: 50% 39.04 / 38.93, 75% 38.54 / 38.79, 25% 39.28 / 38.97).
   // defer_from is a multiple of 64 (wave-uniform).
   const bool deferrable = !d.split || d.msm;
-  const int pct = !deferrable ? 0 : (k.defer_pct >= 0 ? k.defer_pct : (!d.split && d.pairs_per_item == 2 ? 50 : 100));
+  const int pct = !deferrable ? 0 : (k.defer_pct >= 0 ? k.defer_pct : (!d.split && d.pairs_per_item == 2 ? 75 : 100));
   d.defer_grp = pct > 0 ? 1u : 0u;
   d.defer_from = pct > 0 ? (uint32_t)(((uint64_t)n * (uint32_t)(100 - pct) / 100u) & ~63ull) : n;
   // two-level per-job fold (bgv_tail.hip) when few jobs of >= 64 sets leave

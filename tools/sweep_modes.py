@@ -66,6 +66,8 @@ MODES = {  # bgv_cfg overrides (include/bgv.h)
     "msm2": {"msm": 2},
     "nodefer": {"defer_pct": 0},
     "d75": {"defer_pct": 75},
+    "d25": {"defer_pct": 25},
+    "d0": {"defer_pct": 0},
 }
 
 
