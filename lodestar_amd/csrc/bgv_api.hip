@@ -480,9 +480,12 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   //    18,000; the three-lane cofactor clearing from 9,000; sum r_i sigma_i
   //    by the (job, window, digit)-lane MSM from 9,000 (bulk batches: the
   //    (job, window) one)
-  //    (12,544: 18.4 -> 10.6 ms; 25,088: 24.1 -> 16.9 ms; 6,272: 10.8 -> 9.2 ms)
+  //    (12,544: 18.4 -> 10.6 ms; 25,088: 24.1 -> 16.9 ms; 6,272: 10.8 -> 9.2 ms);
+  //    the latency-mode hash (two-lane maps, one-lane clearing) with the
+  //    one-lane Miller loop and the (job, window) MSM up to 65,536 sets
+  //    (37,632: 25.1 -> 22.5 ms; 50,176: 26.0 -> 24.9 ms)
   static const uint32_t MILLER18_MIN = 2000, MILLER4_MIN = 6000, MILLER2_MIN = 18000, MILLER1_MIN = 35000,
-                        MSM_MIN = 6000, MSM4_MIN = 9000, SPLIT_MAX = 35000, PAIRS2_MIN = 65536,
+                        MSM_MIN = 6000, MSM4_MIN = 9000, MSM2_MIN = 35000, SPLIT_MAX = 65536, PAIRS2_MIN = 65536,
                         CLEAR3_MIN = 9000;
   const bgv_cfg& k = c->cfg;
   d.pairs_per_item = k.pairs ? (uint32_t)k.pairs : (n >= PAIRS2_MIN ? 2u : 1u);
@@ -499,7 +502,7 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   {
     uint32_t auto_msm = 0;
     if (n >= MSM_MIN && d.span_log2 <= 8) {
-      if (!d.split) auto_msm = 2;
+      if (!d.split || n >= MSM2_MIN) auto_msm = 2;
       else auto_msm = n < MSM4_MIN ? 1 : 4;
     }
     d.msm = k.msm >= 0 ? (uint32_t)k.msm : auto_msm;

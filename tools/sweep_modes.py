@@ -67,6 +67,11 @@ MODES = {  # bgv_cfg overrides (include/bgv.h)
     "nodefer": {"defer_pct": 0},
     "d75": {"defer_pct": 75},
     "d25": {"defer_pct": 25},
+    "s1m2c1m4": {"split": 1, "miller": 2, "clear_lanes": 1, "msm": 4},
+    "s1m1c1m4": {"split": 1, "miller": 1, "clear_lanes": 1, "msm": 4},
+    "s1m1c1m2": {"split": 1, "miller": 1, "clear_lanes": 1, "msm": 2},
+    "s0m2": {"split": 0, "miller": 2},
+    "s0m4msm": {"split": 0, "msm": 4},
     "d0": {"defer_pct": 0},
 }
 
