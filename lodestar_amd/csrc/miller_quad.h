@@ -16,8 +16,8 @@
 //      P2 = F1 b1 v, P3 = (F0 + F1)(a0 + (a1 + b1) v) on half 1, plus X'^2
 // Operands come from per-pair LDS slots through lane-dependent addresses (a
 // free selection); a wave's LDS accesses execute in issue order, so only the
-// compiler must keep them in order (coop_wave_sync).  The addition steps run
-// redundantly on all four lanes.  Every field value is fully reduced, so f is
+// compiler must keep them in order (coop_wave_sync).  The five addition steps
+// spread their products over the lanes too (quad_add).  Every field value is fully reduced, so f is
 // bit-identical to miller_loop().
 #pragma once
 #include "miller_coop.h"
@@ -290,6 +290,68 @@ __device__ __forceinline__ void quad_line(fp6_t& fh, fp2_t& x2, const g2p_t& T, 
   duo_sel6(fh, h != 0, o1, o0);
 }
 
+// one exchange round: every lane publishes r at slot rho, then reads all four
+__device__ __forceinline__ void quad_round(fp2_t out[4], const fp2_t& r, uint32_t rho, quad_x_t& X) {
+  coop_wave_sync();  // earlier reads of these slots are done
+  X.R[rho] = r;
+  coop_wave_sync();
+  out[0] = X.R[0];
+  out[1] = X.R[1];
+  out[2] = X.R[2];
+  out[3] = X.R[3];
+}
+
+// the addition step (pairing.h miller_add_core<true>, same formulas and
+// values) with its products spread over the four lanes: 3 + 3 + 3 + 2 + 3 Fp
+// products of chain instead of ~37 on every lane.  Leaves T + Q in T and the
+// line (a0, a1, b1, a1 + b1) in X.L.
+__device__ __forceinline__ void quad_add(g2p_t& T, const g2a& Q, const fp_t& xp, const fp_t& yp, uint32_t rho,
+                                         quad_x_t& X) {
+  fp2_t o[4], r;
+  // R1: yQ Z | xQ Z
+  fp2_mul(r, q_sel2((rho & 1u) != 0, Q.x, Q.y), T.z);
+  quad_round(o, r, rho, X);
+  fp2_t th, la;
+  fp2_sub(th, T.y, o[0]);  // theta = Y - yQ Z
+  fp2_sub(la, T.x, o[1]);  // lambda = X - xQ Z
+  // R2: th xQ | la yQ | C = th^2 | D = la^2
+  fp2_mul(r, q_sel4(rho, th, la, th, la), q_sel4(rho, Q.x, Q.y, th, la));
+  quad_round(o, r, rho, X);
+  fp2_t a0, C, D;
+  fp2_sub(a0, o[0], o[1]);
+  C = o[2];
+  D = o[3];
+  // R3: E = D la | F = Z C | G = X D
+  fp2_mul(r, q_sel4(rho, D, T.z, T.x, D), q_sel4(rho, la, C, D, la));
+  quad_round(o, r, rho, X);
+  const fp2_t E = o[0], F = o[1], G = o[2];
+  // R3b: th xP | la yP
+  fp2_mul_fp(r, q_sel2((rho & 1u) != 0, la, th), (rho & 1u) ? yp : xp);
+  quad_round(o, r, rho, X);
+  fp2_t a1, b1, H, gh;
+  fp2_neg(a1, o[0]);
+  b1 = o[1];
+  fp2_add(H, E, F);
+  fp2_sub(H, H, G);
+  fp2_sub(H, H, G);
+  fp2_sub(gh, G, H);
+  // R4: X' = la H | th (G - H) | Y E | Z' = Z E
+  fp2_mul(r, q_sel4(rho, la, th, T.y, T.z), q_sel4(rho, H, gh, E, E));
+  quad_round(o, r, rho, X);
+  T.x = o[0];
+  fp2_sub(T.y, o[1], o[2]);
+  T.z = o[3];
+  fp2_t ab;
+  fp2_add(ab, a1, b1);
+  coop_wave_sync();
+  if (rho == 0) {
+    X.L[0] = a0;
+    X.L[1] = a1;
+    X.L[2] = b1;
+    X.L[3] = ab;
+  }
+}
+
 // the pair (P, Q) on lanes 4k .. 4k+3: fh = this lane's half of f_{x,Q}(P)
 // for the negative x (conjugated)
 __device__ void quad_miller(fp6_t& fh, const g1a& P, const g2a& Q, uint32_t h, uint32_t s, quad_x_t& X) {
@@ -325,17 +387,7 @@ __device__ void quad_miller(fp6_t& fh, const g1a& P, const g2a& Q, uint32_t h, u
       quad_line(fh, x2, T, h, s, rho, X);
     }
     if ((BLS_X_ABS >> bit) & 1ull) {
-      fp2_t a0, a1, b1;
-      miller_add_core<true>(T, a0, a1, b1, Q, P.x, P.y);  // all lanes, same values
-      fp2_t ab;
-      fp2_add(ab, a1, b1);
-      coop_wave_sync();
-      if (rho == 0) {
-        X.L[0] = a0;
-        X.L[1] = a1;
-        X.L[2] = b1;
-        X.L[3] = ab;
-      }
+      quad_add(T, Q, P.x, P.y, rho, X);
       quad_line(fh, x2, T, h, s, rho, X);
     }
   }
