@@ -369,15 +369,15 @@ def test_signature_msm_bit_identical_to_per_set_scaling():
 
 @pytest.mark.gpu
 def test_latency_split_mode_bit_identical():
-    """Latency mode (bgv_cfg.split = 1, default below 35,000 sets: two map lanes
+    """Latency mode (bgv_cfg.split = 1, default below 65,536 sets: two map lanes
     per message, subgroup check beside [r_i] sigma_i) and the one-lane-per-set
     kernels (split = 0) give the same batch partial, byte for byte, and the
     same per-job verdicts and set codes on the golden jobs (which include
     off-curve and out-of-subgroup signatures)."""
     from lodestar_amd import native
     outs = {}
-    for mode in ("0", "1", "1c3"):
-        d = native.Device(0, split=int(mode[0]), **({"clear_lanes": 3} if mode == "1c3" else {}))
+    for mode in ("0", "1", "1c3", "1c1"):  # cofactor clearing on 9 / 3 / 1 lanes per point
+        d = native.Device(0, split=int(mode[0]), **({"clear_lanes": int(mode[2])} if len(mode) > 1 else {}))
         try:
             G.load_golden_table(d)
             a, expected, codes = G.golden_arrays([0, 1, 9, 11, 12, 13], scalars_seed=3)
@@ -391,8 +391,8 @@ def test_latency_split_mode_bit_identical():
             outs[mode] = (part, ok, jr.tolist(), sc.tolist(), jr2.tolist(), bad)
         finally:
             d.close()
-    assert outs["0"][0] == outs["1"][0] == outs["1c3"][0]
-    assert outs["0"][1:5] == outs["1"][1:5] == outs["1c3"][1:5]
+    assert outs["0"][0] == outs["1"][0] == outs["1c3"][0] == outs["1c1"][0]
+    assert outs["0"][1:5] == outs["1"][1:5] == outs["1c3"][1:5] == outs["1c1"][1:5]
     assert outs["1"][2] == gexp and outs["1"][3] == gcodes
     assert outs["1"][4] == np.where(outs["1"][5], 0, 1).tolist()
 

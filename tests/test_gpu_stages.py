@@ -31,6 +31,8 @@ MODES = {
     "quad_msm0_clear3": {"miller": 4, "msm": 0, "clear_lanes": 3},
     "quad_split_msm4": {"miller": 4, "msm": 4, "split": 1, "clear_lanes": 3},
     "quad_split_msm3": {"miller": 4, "msm": 3, "split": 1, "clear_lanes": 3},
+    "split_one_lane_miller_msm2": {"split": 1, "miller": 1, "msm": 2, "clear_lanes": 1},
+    "duo_clear1_msm4": {"split": 1, "miller": 2, "msm": 4, "clear_lanes": 1},
     "bulk": {"split": 0},
     "bulk_serial_msm": {"split": 0, "miller": 1, "msm": 1, "pairs": 1},
     "c4_path": {"split": 0, "miller": 1, "msm": 2, "pairs": 2},
