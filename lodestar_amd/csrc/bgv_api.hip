@@ -578,7 +578,7 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
   if ((r = c->sig_aff.ensure(ns)) || (r = c->h_aff.ensure(ns)) || (r = c->sig_inf.ensure(ns)) ||
       (r = c->sig_code.ensure(ns)) || (r = c->pk_code.ensure(ns)) || (r = c->rpk_aff.ensure(ns)) ||
       (r = c->rsig.ensure(ns)) || (r = c->f_set.ensure(ns + nj)) || (r = c->set_code.ensure(ns)) ||
-      (r = c->set_job.ensure(ns)) || (r = c->item_off.ensure(nj + 1)) || (r = c->item_job.ensure(ns + nj + 1)) || (r = c->f_job.ensure(nj)) || (r = c->f_batch.ensure(nj)) || (r = c->f_tmp.ensure(nj / 32 + 1)) ||
+      (r = c->set_job.ensure(ns)) || (r = c->item_off.ensure(nj + 1)) || (r = c->item_job.ensure(ns + nj + 1)) || (r = c->f_job.ensure(nj)) || (r = c->f_batch.ensure(nj)) || (r = c->f_tmp.ensure(nj / 8 + 1)) ||
       (r = c->s_aff.ensure(nj)) || (r = c->s_inf.ensure(nj)) || (r = c->job_code.ensure(nj)) ||
       (r = c->job_result.ensure(nj)) || (r = c->f_part.ensure(4)) || (r = c->flags.ensure(8)))
     return r;

@@ -72,7 +72,7 @@ struct dev_work {
   fp12_t* f_set;      // per pair Miller value: n_sets set pairs, then n_jobs (-G1, S_job) pairs
   fp12_t* f_job;      // per-job Miller product (incl. the -G1 pair)
   fp12_t* f_batch;    // batch product scratch [n_jobs]; the product ends in f_batch[0]
-  fp12_t* f_tmp;      // batch fold ping-pong [ceil(n_jobs / 32)]
+  fp12_t* f_tmp;      // batch fold ping-pong [ceil(n_jobs / 8)]
   int32_t* job_code;
   int32_t* job_result;
   int32_t* set_code;

@@ -98,12 +98,15 @@ __global__ void COOP_LB k_job_fold(dev_batch b, dev_work w, uint32_t stride) {
   c_store(w.f_batch[j], &acc);
 }
 
-// workgroup g: dst[g] = prod src[32 g .. min(n, 32 g + 32)); with one
-// workgroup dst may alias src (every read precedes the write)
-__global__ void COOP_LB k_fold32(const fp12_t* src, uint32_t n, fp12_t* dst) {
+// workgroup g: dst[g] = prod src[F g .. min(n, F g + F)) with fan-in F; with
+// one workgroup dst may alias src (every read precedes the write).  A
+// fan-in of 8 keeps the chain of sequential Fp12 products short: 1,024 job
+// values fold in 8 + 8 + 8 + 8 + 2 products instead of 32 + 32.
+constexpr uint32_t FOLD_FAN = 8;
+__global__ void COOP_LB k_fold(const fp12_t* src, uint32_t n, fp12_t* dst) {
   __shared__ cscratch s;
   __shared__ wfp12 acc, x;
-  const uint32_t beg = blockIdx.x * 32u, end = min(n, beg + 32u);
+  const uint32_t beg = blockIdx.x * FOLD_FAN, end = min(n, beg + FOLD_FAN);
   c_load(&acc, src[beg]);
   for (uint32_t i = beg + 1; i < end; i++) {
     c_load(&x, src[i]);
@@ -187,17 +190,17 @@ void launch_fp12_tail(hipStream_t st, int stage, const dev_batch& b, const dev_w
       for (uint32_t s = 1; s < span; s *= 2) hipLaunchKernelGGL(k_f_level, grid(b.n_sets), dim3(64), 0, st, b, w, s);
     hipLaunchKernelGGL(k_job_f, grid(b.n_jobs), dim3(64), 0, st, b, w, span);
   } else if (stage == ST_BATCH_PROD) {
-    // fold by 32, ping-ponging f_batch <-> f_tmp, the product landing in f_batch[0]
+    // fold by FOLD_FAN, ping-ponging f_batch <-> f_tmp, the product landing in f_batch[0]
     uint32_t n = b.n_jobs;
     fp12_t* src = w.f_batch;
-    while (n > 32) {
+    while (n > FOLD_FAN) {
       fp12_t* dst = src == w.f_batch ? w.f_tmp : w.f_batch;
-      const uint32_t groups = (n + 31) / 32;
-      hipLaunchKernelGGL(k_fold32, dim3(groups), ct, 0, st, src, n, dst);
+      const uint32_t groups = (n + FOLD_FAN - 1) / FOLD_FAN;
+      hipLaunchKernelGGL(k_fold, dim3(groups), ct, 0, st, src, n, dst);
       src = dst;
       n = groups;
     }
-    if (n > 1 || (n == 1 && src != w.f_batch)) hipLaunchKernelGGL(k_fold32, dim3(1), ct, 0, st, src, n, w.f_batch);
+    if (n > 1 || (n == 1 && src != w.f_batch)) hipLaunchKernelGGL(k_fold, dim3(1), ct, 0, st, src, n, w.f_batch);
   } else if (stage == ST_BATCH_FINAL) {
     hipLaunchKernelGGL(k_batch_final, dim3(1), ct, 0, st, b, w);
   } else if (stage == ST_JOB_FINAL) {
