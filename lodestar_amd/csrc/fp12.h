@@ -118,6 +118,28 @@ BGV_NI6 void fp6_mul_1(fp6_t& r, const fp6_t& a, const fp2_t& b1) {
   r.c0 = c0; r.c1 = c1; r.c2 = c2;
 }
 
+// a * (b1 v + b2 v^2): 5 Fp2 products
+BGV_NI6 void fp6_mul_12(fp6_t& r, const fp6_t& a, const fp2_t& b1, const fp2_t& b2) {
+  fp2_t t1, t2, u, s0, s1, c0, c1, c2;
+  F6_MUL(t1, a.c1, b1);
+  F6_MUL(t2, a.c2, b2);
+  // c0 = xi (a1 b2 + a2 b1) = xi ((a1+a2)(b1+b2) - t1 - t2)
+  fp2_add(s0, a.c1, a.c2);
+  fp2_add(s1, b1, b2);
+  F6_MUL(u, s0, s1);
+  fp2_sub(u, u, t1);
+  fp2_sub(u, u, t2);
+  fp2_mul_xi(c0, u);
+  // c1 = a0 b1 + xi t2
+  F6_MUL(u, a.c0, b1);
+  fp2_mul_xi(t2, t2);
+  fp2_add(c1, u, t2);
+  // c2 = a0 b2 + t1
+  F6_MUL(u, a.c0, b2);
+  fp2_add(c2, u, t1);
+  r.c0 = c0; r.c1 = c1; r.c2 = c2;
+}
+
 BGV_NI void fp6_inv(fp6_t& r, const fp6_t& a) {
   // c0 = a0^2 - xi a1 a2, c1 = xi a2^2 - a0 a1, c2 = a1^2 - a0 a2
   fp2_t c0, c1, c2, t;
@@ -194,6 +216,51 @@ BGV_NI12 void fp12_mul_line(fp12_t& r, const fp12_t& f, const fp2_t& a0, const f
   fp6_mul_01(s, s, a0, a1b1);
   fp6_sub(s, s, t0);
   fp6_sub(r.c1, s, t1);
+  fp6_mul_v(t1, t1);
+  fp6_add(r.c0, t0, t1);
+}
+
+// f * l * l' for two sparse lines l = a0 + a1 w^2 + b1 w^3, l' = c0 + c1 w^2 + d1 w^3
+// (the two pairs of one multi-Miller step): the lines are multiplied first,
+//   l l' = (a0c0 + xi b1d1, a0c1 + a1c0, a1c1) + (0, a0d1 + b1c0, a1d1 + b1c1) w
+// (6 Fp2 products), then f by that five-term element (6 + 5 + 6): 23 Fp2
+// products against 26 for two fp12_mul_line, and f is read and written once
+BGV_NI12 void fp12_mul_line2(fp12_t& r, const fp12_t& f, const fp2_t& a0, const fp2_t& a1, const fp2_t& b1,
+                             const fp2_t& c0, const fp2_t& c1, const fp2_t& d1) {
+  fp2_t ac0, ac1, bd, s, u;
+  fp6_t x;
+  fp2_t y1, y2;
+  F6_MUL(ac0, a0, c0);
+  F6_MUL(ac1, a1, c1);
+  F6_MUL(bd, b1, d1);
+  fp2_mul_xi(u, bd);
+  fp2_add(x.c0, ac0, u);
+  fp2_add(s, a0, a1);
+  fp2_add(u, c0, c1);
+  F6_MUL(x.c1, s, u);
+  fp2_sub(x.c1, x.c1, ac0);
+  fp2_sub(x.c1, x.c1, ac1);
+  x.c2 = ac1;
+  fp2_add(s, a0, b1);
+  fp2_add(u, c0, d1);
+  F6_MUL(y1, s, u);
+  fp2_sub(y1, y1, ac0);
+  fp2_sub(y1, y1, bd);
+  fp2_add(s, a1, b1);
+  fp2_add(u, c1, d1);
+  F6_MUL(y2, s, u);
+  fp2_sub(y2, y2, ac1);
+  fp2_sub(y2, y2, bd);
+  // f (x + y w) with y = y1 v + y2 v^2
+  fp6_t t0, t1, sf;
+  fp6_mul(t0, f.c0, x);
+  fp6_mul_12(t1, f.c1, y1, y2);
+  fp6_add(sf, f.c0, f.c1);
+  fp2_add(x.c1, x.c1, y1);
+  fp2_add(x.c2, x.c2, y2);
+  fp6_mul(sf, sf, x);
+  fp6_sub(sf, sf, t0);
+  fp6_sub(r.c1, sf, t1);
   fp6_mul_v(t1, t1);
   fp6_add(r.c0, t0, t1);
 }

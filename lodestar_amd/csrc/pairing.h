@@ -21,6 +21,11 @@
 #else
 #define BGV_NIL BGV_NI
 #endif
+// the two-pair loops multiply each step's two lines together before f
+// (fp12_mul_line2: 23 Fp2 products per step instead of 26)
+#ifndef BGV_MILLER_LINE2
+#define BGV_MILLER_LINE2 1
+#endif
 
 namespace bgv {
 
@@ -214,20 +219,35 @@ BGV_NIL void miller_loop2(fp12_t& f, const g1a& P1, const g2a& Q1, const g1a& P2
   for (int b = 62; b >= 0; b--) {
     if (b != 62) fp12_sqr(f, f);
     miller_dbl_step(T1, a0, a1, b1, P1.x, P1.y);
-    if (b == 62) {  // f = 1 * line
-      f.c0.c0 = a0;
-      f.c0.c1 = a1;
-      f.c1.c1 = b1;
-    } else {
+#if BGV_MILLER_LINE2
+    if (b != 62) {
+      fp2_t c0, c1, d1;
+      miller_dbl_step(T2, c0, c1, d1, P2.x, P2.y);
+      fp12_mul_line2(f, f, a0, a1, b1, c0, c1, d1);
+    } else
+#endif
+    {
+      if (b == 62) {  // f = 1 * line
+        f.c0.c0 = a0;
+        f.c0.c1 = a1;
+        f.c1.c1 = b1;
+      } else {
+        fp12_mul_line(f, f, a0, a1, b1);
+      }
+      miller_dbl_step(T2, a0, a1, b1, P2.x, P2.y);
       fp12_mul_line(f, f, a0, a1, b1);
     }
-    miller_dbl_step(T2, a0, a1, b1, P2.x, P2.y);
-    fp12_mul_line(f, f, a0, a1, b1);
     if ((BLS_X_ABS >> b) & 1ull) {
       miller_add_step(T1, a0, a1, b1, Q1, P1.x, P1.y);
+#if BGV_MILLER_LINE2
+      fp2_t c0, c1, d1;
+      miller_add_step(T2, c0, c1, d1, Q2, P2.x, P2.y);
+      fp12_mul_line2(f, f, a0, a1, b1, c0, c1, d1);
+#else
       fp12_mul_line(f, f, a0, a1, b1);
       miller_add_step(T2, a0, a1, b1, Q2, P2.x, P2.y);
       fp12_mul_line(f, f, a0, a1, b1);
+#endif
     }
   }
   fp12_conj(f, f);  // x < 0
@@ -242,24 +262,42 @@ BGV_NIL void miller_loop_lines(fp12_t& f, const fp2_t* lines, uint32_t stride, c
   for (int b = 62; b >= 0; b--) {
     if (b != 62) fp12_sqr(f, f);
     miller_line_at_p(a0, a1, b1, lines, stride, i1, s, false, P1.x, P1.y);
-    if (b == 62) {  // f = 1 * line
-      f.c0.c0 = a0;
-      f.c0.c1 = a1;
-      f.c1.c1 = b1;
-    } else {
-      fp12_mul_line(f, f, a0, a1, b1);
-    }
-    if (two) {
-      miller_line_at_p(a0, a1, b1, lines, stride, i2, s, false, P2.x, P2.y);
-      fp12_mul_line(f, f, a0, a1, b1);
+#if BGV_MILLER_LINE2
+    if (two && b != 62) {
+      fp2_t c0, c1, d1;
+      miller_line_at_p(c0, c1, d1, lines, stride, i2, s, false, P2.x, P2.y);
+      fp12_mul_line2(f, f, a0, a1, b1, c0, c1, d1);
+    } else
+#endif
+    {
+      if (b == 62) {  // f = 1 * line
+        f.c0.c0 = a0;
+        f.c0.c1 = a1;
+        f.c1.c1 = b1;
+      } else {
+        fp12_mul_line(f, f, a0, a1, b1);
+      }
+      if (two) {
+        miller_line_at_p(a0, a1, b1, lines, stride, i2, s, false, P2.x, P2.y);
+        fp12_mul_line(f, f, a0, a1, b1);
+      }
     }
     s++;
     if ((BLS_X_ABS >> b) & 1ull) {
       miller_line_at_p(a0, a1, b1, lines, stride, i1, s, true, P1.x, P1.y);
-      fp12_mul_line(f, f, a0, a1, b1);
+#if BGV_MILLER_LINE2
       if (two) {
-        miller_line_at_p(a0, a1, b1, lines, stride, i2, s, true, P2.x, P2.y);
+        fp2_t c0, c1, d1;
+        miller_line_at_p(c0, c1, d1, lines, stride, i2, s, true, P2.x, P2.y);
+        fp12_mul_line2(f, f, a0, a1, b1, c0, c1, d1);
+      } else
+#endif
+      {
         fp12_mul_line(f, f, a0, a1, b1);
+        if (two) {
+          miller_line_at_p(a0, a1, b1, lines, stride, i2, s, true, P2.x, P2.y);
+          fp12_mul_line(f, f, a0, a1, b1);
+        }
       }
       s++;
     }
