@@ -757,6 +757,7 @@ __global__ void BGV_BULK k_set_job(dev_batch b, dev_work w) {
   for (uint32_t i = b.job_off[j]; i < b.job_off[j + 1]; i++) w.set_job[i] = j;
 }
 
+constexpr uint32_t S_COOP_MAX = 16384;  // ST_S_TREE: k_s_level_coop below, k_s_level above
 __global__ void BGV_BULK k_s_level(dev_batch b, dev_work w, uint32_t s) {
   const uint32_t i = gtid();
   if (i >= b.n_sets) return;
@@ -1219,7 +1220,11 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
         BGV_LAUNCH(k_job_code, b.n_jobs, b, w);
         break;
       }
-      for (uint32_t s = 1; s < span; s *= 2) BGV_LAUNCH(k_s_level, b.n_sets, b, w, s);
+      // nine lanes per addition while the first level's groups fit the SIMDs
+      for (uint32_t s = 1; s < span; s *= 2) {
+        if (BGV_COOP_G2 && b.n_sets < S_COOP_MAX) launch_s_level_coop(st, b, w, s);  // bgv_latency.hip
+        else BGV_LAUNCH(k_s_level, b.n_sets, b, w, s);
+      }
       BGV_LAUNCH(k_job_s, b.n_jobs, b, w, span);
       break;
     case ST_MILLER:  // (r_i PK_i, H(m_i)) pairs: needs ST_HASH and ST_PK only

@@ -95,6 +95,31 @@ void launch_hash_clear_trio(hipStream_t st, const dev_batch& b, const dev_work& 
   if (b.n_sets) hipLaunchKernelGGL(k_hash_clear_trio, dim3((b.n_sets + CG3_GROUPS - 1) / CG3_GROUPS), dim3(64), 0, st, b, w);
 }
 
+// One level of the per-job signature sum (bgv_kernels.hip k_s_level) on nine
+// lanes per addition (coop_g2.h cg_add, 6 rounds of one Fp product):
+// rsig[i] += rsig[i + s] for every set i an even multiple of s past its job's
+// start.  A one-lane G2 addition costs ~140 us of latency (k_s_level: 0.15 ms
+// per level at 3,136 sets); waves without a live addition leave at once.
+__global__ void __launch_bounds__(64, 1) k_s_level_coop(dev_batch b, dev_work w, uint32_t s) {
+  __shared__ cg_scratch sm[CG_GROUPS + 1];
+  const uint32_t lane = threadIdx.x, grp = lane / CG_LANES, r9 = lane % CG_LANES, sl = r9 / 3, q = r9 % 3;
+  const uint32_t i0 = blockIdx.x * CG_GROUPS + grp;
+  bool own = grp < CG_GROUPS && i0 < b.n_sets;
+  if (own) {
+    const uint32_t j = w.set_job[i0];
+    own = ((i0 - b.job_off[j]) % (2u * s)) == 0 && i0 + s < b.job_off[j + 1];
+  }
+  if (!__any(own)) return;  // wave-uniform
+  const uint32_t i = own ? i0 : 0u, k = own ? i0 + s : 0u;
+  g2j r;
+  cg_add<3>(&sm[grp], sl, q, r, w.rsig[i], w.rsig[k]);
+  if (own && sl == 0 && q == 0) w.rsig[i] = r;
+}
+
+void launch_s_level_coop(hipStream_t st, const dev_batch& b, const dev_work& w, uint32_t s) {
+  if (b.n_sets) hipLaunchKernelGGL(k_s_level_coop, dim3((b.n_sets + CG_GROUPS - 1) / CG_GROUPS), dim3(64), 0, st, b, w, s);
+}
+
 void launch_sig_split_coop(hipStream_t st, const dev_batch& b, const dev_work& w) {
   if (b.n_sets) hipLaunchKernelGGL(k_sig_split_coop, dim3(2u * ((b.n_sets + CG_GROUPS - 1) / CG_GROUPS)), dim3(64), 0, st, b, w);
 }
