@@ -498,6 +498,7 @@ def main():
     value = total_sets * args.steps / elapsed
 
     stage_ms = {d.stage_name(i): float(stage_sum[i] / args.steps) for i in range(native.N_STAGES) if d.stage_name(i) != "unknown"}
+    timed_layout = d.last_stats.layout()  # the variant the timed batches ran with (bgv_stats), before the extra legs
 
     legs = {}
     if shard and not args.no_weak_leg:
@@ -526,7 +527,7 @@ def main():
         fpm_rate = 256 * 256 * 8 * 2048 / (fpm_ms * 1e-3) / 1e9
         per_stage = {}
         stage_counts = dict(counts["per_set"]) if counts else {}
-        lay = d.last_stats.layout()  # the variant the timed batches ran with (bgv_stats)
+        lay = timed_layout
         if counts and lay["lines"] and "per_set_lines" in counts:
             stage_counts["miller_loop"] = counts["per_set_lines"]["miller_loop"]
         share = (n_sets - min(lay["defer_from"], n_sets)) / max(n_sets, 1)
