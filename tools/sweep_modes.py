@@ -73,6 +73,11 @@ MODES = {  # bgv_cfg overrides (include/bgv.h)
     "s0m2": {"split": 0, "miller": 2},
     "s0m4msm": {"split": 0, "msm": 4},
     "d0": {"defer_pct": 0},
+    "d50": {"defer_pct": 50},
+    "d100": {"defer_pct": 100},
+    "nolines": {"lines": 0},
+    "p2": {"pairs": 2},
+    "p2l": {"pairs": 2, "lines": 1},
 }
 
 
