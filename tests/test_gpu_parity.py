@@ -367,6 +367,36 @@ def test_signature_msm_bit_identical_to_per_set_scaling():
     assert outs["0"] == outs["1"] == outs["2"] == outs["3"] == outs["4"]
 
 
+def test_signature_tree_large_jobs_bit_identical():
+    """Jobs of 300 and 200 sets (a nine-level S_job tree, past the 256-set span
+    of the MSM defaults) summed by the nine-lane tree levels (msm 0 below
+    16,384 sets, k_s_level_coop) and by the (job, window) MSM: same batch
+    partial, byte for byte, and the verdicts of a clean and a faulted job."""
+    from lodestar_amd import native
+    outs = {}
+    for mode in (0, 2):
+        d = native.Device(0, msm=mode)
+        try:
+            G.load_golden_table(d)
+            first = d.pubkeys_count()
+            d.gen_keys(first, 256, 7)
+            syn, bad = _synthetic_on(d, 500, 4, first, 256, 9, fault_every=0)
+            syn["n_jobs"] = 2
+            syn["job_offsets"] = np.array([0, 300, 500], np.uint32)
+            part, _, _, ok = d.partial(syn)
+            jr, _ = d.verify(syn)
+            assert jr.tolist() == [1, 1] and ok
+            faulted, _ = _synthetic_on(d, 500, 4, first, 256, 9, fault_every=211)
+            faulted["n_jobs"] = 2
+            faulted["job_offsets"] = np.array([0, 300, 500], np.uint32)
+            jr2, _ = d.verify(faulted)
+            assert jr2.tolist() == [0, 0]  # sets 0 and 211 (job 0), 422 (job 1)
+            outs[mode] = part
+        finally:
+            d.close()
+    assert outs[0] == outs[2]
+
+
 @pytest.mark.gpu
 def test_latency_split_mode_bit_identical():
     """Latency mode (bgv_cfg.split = 1, default below 65,536 sets: two map lanes
