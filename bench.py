@@ -208,11 +208,12 @@ def golden_fault_sigs():
     raise RuntimeError("no not-in-G2 vector in the golden file")
 
 
-def inject_faults(d, arrays: dict, rate: float, seed: int):
+def inject_faults(d, arrays: dict, rate: float, seed: int, with_codes: bool = False):
     """C5: `rate` of the sets faulted, a quarter each of wrong-message
     signature (-> false), swapped pubkey index (-> false), cleared compression flag
     (-> reject BLST_BAD_ENCODING) and an on-curve point outside G2 (-> reject
-    BLST_POINT_NOT_IN_GROUP).  Returns (arrays with sigs, expected per-job results)."""
+    BLST_POINT_NOT_IN_GROUP).  Returns (arrays with sigs, expected per-job results)
+    and, with_codes, the expected per-set codes."""
     n, nj = arrays["n_sets"], arrays["n_jobs"]
     rng = np.random.default_rng(seed)
     pick = np.sort(rng.choice(n, size=max(4, int(n * rate)), replace=False))
@@ -241,6 +242,8 @@ def inject_faults(d, arrays: dict, rate: float, seed: int):
         c = code[jo[j]:jo[j + 1]]
         nz = np.nonzero(c)[0]
         expect.append(-int(c[nz[0]]) if len(nz) else (0 if false_set[jo[j]:jo[j + 1]].any() else 1))
+    if with_codes:
+        return out, np.array(expect, np.int32), code
     return out, np.array(expect, np.int32)
 
 
@@ -279,6 +282,8 @@ def small_configs(d, torch, dev, arrays):
     out["c1_singles_latency_ms"] = {"p50": p50_latency(d, signed(d, singles(128, SEED + 3000))), "sets": 128}
     # one set (verifyOnMainThread gossip block proposer, chain/validation/block.ts:146)
     out["single_set_latency_ms"] = {"p50": p50_latency(d, signed(d, singles(1, SEED + 3500))), "sets": 1}
+    # verifyMultipleSignatures of 3 / 8 / 32 single sets (test/perf/bls/bls.test.ts:43-53)
+    out["small_batch_latency_ms"] = {str(k): p50_latency(d, signed(d, singles(k, SEED + 3600 + k))) for k in (3, 8, 32)}
     # C5: the C4 segment with 1% faults; the batch check fails, so every block takes
     # the per-job final exponentiation (worker retry, multithread/worker.ts:74-85)
     c5a, c5_expect = inject_faults(d, arrays, 0.01, SEED + 4000)
@@ -334,12 +339,13 @@ def shard_projection(d, torch, dev, arrays_host: dict, worlds=(2, 4, 8), reps: i
     `world` partials (bgv_combine_final).  ms = median partial + combine; the
     RCCL all-gather of 576 B per rank is not included (latency-bound, ~tens of
     us over xGMI).  projected_sets_per_s = 100,352 / ms."""
-    from lodestar_amd.dist import select_jobs, shard_jobs
-    jo = arrays_host["job_offsets"]
-    sizes = [int(jo[j + 1] - jo[j]) for j in range(arrays_host["n_jobs"])]
+    from lodestar_amd.dist import batch_job_work, select_jobs, shard_balance, shard_jobs
+    work = batch_job_work(arrays_host)
     out = {}
     for world in worlds:
-        ids = shard_jobs(sizes, world)[0]
+        shards = shard_jobs(work, world)
+        # the heaviest shard sets the node's time
+        ids = max(shards, key=lambda s: sum(work[j] for j in s))
         sub = to_device(select_jobs(arrays_host, ids), torch, dev)
         sub["scalars"] = None
         part, _, jr, ok = d.partial(sub, on_device=True)
@@ -353,6 +359,7 @@ def shard_projection(d, torch, dev, arrays_host: dict, worlds=(2, 4, 8), reps: i
             t.append(time.perf_counter() - t1)
         ms = float(np.median(t)) * 1e3
         out[f"c4_over_{world}"] = {"sets_per_rank": int(sub["n_sets"]), "ms": round(ms, 3),
+                                  "work_max_over_mean": round(shard_balance(work, shards), 4),
                                   "projected_sets_per_s": round(arrays_host["n_sets"] / ms * 1e3, 1)}
     return out
 
@@ -434,7 +441,7 @@ def main():
 
     shard = world > 1 and not args.weak
     from lodestar_amd import native
-    from lodestar_amd.dist import gather_job_results, select_jobs, shard_jobs, verify_sharded
+    from lodestar_amd.dist import batch_job_work, gather_job_results, select_jobs, shard_jobs, verify_sharded
 
     # per-stage timing events: automatic from 65,536 sets; forced for the
     # smaller shards of N > 1 (they would add queue time to the N = 1 latency legs)
@@ -445,7 +452,7 @@ def main():
 
     seg = build_segment(list(range(args.blocks)), seed=SEED + (0 if shard else rank))
     jo = seg["job_offsets"]
-    shards = shard_jobs([int(jo[j + 1] - jo[j]) for j in range(seg["n_jobs"])], world) if shard else None
+    shards = shard_jobs(batch_job_work(seg), world) if shard else None
     arrays = select_jobs(seg, shards[rank]) if shard else seg
     darr = to_device(arrays, torch, dev)
     n_sets = arrays["n_sets"]

@@ -171,6 +171,10 @@ typedef struct bgv_cfg {
 void bgv_cfg_default(bgv_cfg* cfg);
 
 int bgv_abi_version(void);
+/* SHA-256 (hex) of the sources this library was compiled from (csrc + this
+ * header, tools/build.py source_hash); bindings refuse a library whose id
+ * differs from the tree beside it, so a stale build is never run */
+const char* bgv_build_id(void);
 const char* bgv_set_code_name(int code); /* "BLST_BAD_ENCODING", ... */
 const char* bgv_stage_name(int stage);
 const char* bgv_last_error(void);        /* thread-local text of the last failure */

@@ -114,6 +114,7 @@ struct bgv_ctx {
   dbuf<g2j> rsig, q_part;
   dbuf<uint32_t> sig_grp;
   dbuf<fp2_t> lines;
+  uint32_t lines_idle = 0;  // batches in a row that did not use the line buffer
   dbuf<fp12_t> f_set, f_job, f_batch, f_tmp, f_part;
   dbuf<uint32_t> set_job, s_inf, item_off, item_job;
   dbuf<g2a> s_aff;
@@ -127,6 +128,10 @@ struct bgv_ctx {
 // Definitions below take C linkage from their declarations in bgv.h.
 
 int bgv_abi_version(void) { return BGV_ABI_VERSION; }
+#ifndef BGV_SRC_HASH
+#define BGV_SRC_HASH "unhashed"
+#endif
+const char* bgv_build_id(void) { return BGV_SRC_HASH; }
 const char* bgv_last_error(void) { return g_err.c_str(); }
 
 const char* bgv_set_code_name(int code) {
@@ -181,6 +186,14 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
     if (k.clear_lanes != -1 && k.clear_lanes != 1 && k.clear_lanes != 3 && k.clear_lanes != 9)
       return fail(BGV_E_INVALID_ARG, "bgv_cfg.clear_lanes %d", k.clear_lanes);
     if (k.defer_pct < -1 || k.defer_pct > 100) return fail(BGV_E_INVALID_ARG, "bgv_cfg.defer_pct %d", k.defer_pct);
+    auto tri_ok = [](int v) { return v >= -1 && v <= 1; };
+    if (!tri_ok(k.split)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.split %d", k.split);
+    if (!tri_ok(k.prefold)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.prefold %d", k.prefold);
+    if (!tri_ok(k.lines)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.lines %d", k.lines);
+    if (!tri_ok(k.timing)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.timing %d", k.timing);
+    // two pairs per item exist only in the one-lane loop
+    if (k.pairs == 2 && k.miller != -1 && k.miller != 1)
+      return fail(BGV_E_INVALID_ARG, "bgv_cfg.pairs 2 needs the one-lane Miller loop (miller %d)", k.miller);
   }
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(BGV_E_NO_DEVICE, "no HIP device visible");
@@ -567,7 +580,20 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   return 0;
 }
 
+static int work_alloc_once(bgv_ctx* c, const dev_batch& d, dev_work& w);
+
+// a kept line buffer the batch does not use gives way under memory pressure
 static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
+  int r = work_alloc_once(c, d, w);
+  if (r && !d.lines && c->lines.cap) {
+    c->lines.release();
+    c->lines_idle = 0;
+    r = work_alloc_once(c, d, w);
+  }
+  return r;
+}
+
+static int work_alloc_once(bgv_ctx* c, const dev_batch& d, dev_work& w) {
   const uint32_t n = d.n_sets, J = d.n_jobs;
   const size_t ns = n ? n : 1, nj = J ? J : 1;
   int r = 0;
@@ -596,12 +622,19 @@ static int work_alloc(bgv_ctx* c, const dev_batch& d, dev_work& w) {
     if ((r = c->sig_grp.ensure(ns))) return r;
     w.sig_grp = c->sig_grp.p;
   }
+  // the line buffer (19.6 KB per set, 1.3-2.6 GB) stays across batches: a
+  // node alternating gossip batches with range-sync segments would otherwise
+  // hipFree / hipMalloc gigabytes (each free synchronises the device) on every
+  // switch; it goes back after LINES_KEEP batches in a row without lines
+  static const uint32_t LINES_KEEP = 64;
   w.lines = nullptr;
   if (d.lines) {
+    c->lines_idle = 0;
     if ((r = c->lines.ensure((size_t)3 * MILLER_STEPS * ns))) return r;
     w.lines = c->lines.p;
-  } else if (c->lines.cap) {
-    c->lines.release();  // a batch without lines: give the 19.6 KB per set back
+  } else if (c->lines.cap && ++c->lines_idle >= LINES_KEEP) {
+    c->lines.release();
+    c->lines_idle = 0;
   }
   w.msm_bucket = nullptr; w.msm_mask = nullptr; w.msm_win = nullptr;
   if (d.msm == 2) {

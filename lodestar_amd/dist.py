@@ -23,16 +23,53 @@ import numpy as np
 PARTIAL_BYTES = 576
 
 
-def shard_jobs(job_sizes: list[int], world: int) -> list[list[int]]:
-    """Whole jobs to ranks, greedy by set count (largest first), job order kept
-    inside a shard.  A job is never split (its verdict is an AND of its sets)."""
+# Work model for balancing shards (SURVEY 8e "balancing by sum W(k)"): the
+# device cost of a set in Montgomery Fp products, from the instrumented host
+# build of the kernels' headers (tools/opcount.cpp -> tools/fpmul_counts.json):
+# every set pays its signature decode + checks, hash_to_G2, [r]PK, its Miller
+# loop and its share of the signature sum and folds (per_set_total minus the
+# gather, 15,201.7 - 1,411.6); every pubkey reference one G1 mixed addition of
+# the gather (11).  So a 512-key sync aggregate weighs 1.4 single sets and a
+# 98-set block of 128-key aggregates ~109 sets.
+WORK_PER_SET = 13790.0
+WORK_PER_PUBKEY = 11.0
+
+
+def job_work(job_sets, job_refs) -> list[float]:
+    """W(job) = sets * WORK_PER_SET + pubkey references * WORK_PER_PUBKEY"""
+    return [s * WORK_PER_SET + k * WORK_PER_PUBKEY for s, k in zip(job_sets, job_refs)]
+
+
+def batch_job_work(arrays: dict) -> list[float]:
+    """job_work of every job of a bgv_batch (host numpy arrays)"""
+    jo = np.asarray(arrays["job_offsets"], np.int64)
+    po = np.asarray(arrays["pk_offsets"], np.int64)
+    sets = jo[1:] - jo[:-1]
+    refs = po[jo[1:]] - po[jo[:-1]]
+    return job_work(sets.tolist(), refs.tolist())
+
+
+def shard_jobs(job_weights, world: int) -> list[list[int]]:
+    """Whole jobs to ranks, greedy by work (largest first, each to the least
+    loaded rank), job order kept inside a shard.  A job is never split (its
+    verdict is an AND of its sets).  job_weights: batch_job_work / job_work,
+    or set counts."""
     shards: list[list[int]] = [[] for _ in range(world)]
-    load = [0] * world
-    for j in sorted(range(len(job_sizes)), key=lambda j: (-job_sizes[j], j)):
+    load = [0.0] * world
+    w = [float(x) for x in job_weights]
+    floor = min((x for x in w if x > 0), default=1.0)  # an empty job still costs a slot
+    for j in sorted(range(len(w)), key=lambda j: (-w[j], j)):
         r = load.index(min(load))
         shards[r].append(j)
-        load[r] += max(job_sizes[j], 1)
+        load[r] += max(w[j], floor)
     return [sorted(s) for s in shards]
+
+
+def shard_balance(job_weights, shards) -> float:
+    """max over shards of the shard's work / mean shard work (1.0 = even)"""
+    loads = [sum(float(job_weights[j]) for j in s) for s in shards]
+    mean = sum(loads) / max(len(loads), 1)
+    return max(loads) / mean if mean else 1.0
 
 
 def select_jobs(arrays: dict, jobs: list[int]) -> dict:

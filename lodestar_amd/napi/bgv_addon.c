@@ -3,6 +3,7 @@
  * node_api.h (N-API v4+, Node >= 12), no node-addon-api / C++ wrapper.
  *
  *   abiVersion() -> number                      bgv_abi_version
+ *   buildId() -> string                         bgv_build_id
  *   codeName(code) -> "BLST_..."                 bgv_set_code_name
  *   open(device) -> ctx (external)               bgv_open      (multithread/index.ts:120)
  *   close(ctx)                                   bgv_close     (multithread/index.ts:193-214)
@@ -112,6 +113,13 @@ static napi_value AbiVersion(napi_env env, napi_callback_info info) {
   (void)info;
   napi_value r;
   NAPI_CALL(env, napi_create_int32(env, bgv_abi_version(), &r));
+  return r;
+}
+
+static napi_value BuildId(napi_env env, napi_callback_info info) {
+  (void)info;
+  napi_value r;
+  NAPI_CALL(env, napi_create_string_utf8(env, bgv_build_id(), NAPI_AUTO_LENGTH, &r));
   return r;
 }
 
@@ -522,6 +530,7 @@ static napi_value VerifySync(napi_env env, napi_callback_info info) {
 static napi_value Init(napi_env env, napi_value exports) {
   napi_property_descriptor d[] = {
       {"abiVersion", NULL, AbiVersion, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"buildId", NULL, BuildId, NULL, NULL, NULL, napi_enumerable, NULL},
       {"codeName", NULL, CodeName, NULL, NULL, NULL, napi_enumerable, NULL},
       {"open", NULL, Open, NULL, NULL, NULL, napi_enumerable, NULL},
       {"close", NULL, Close, NULL, NULL, NULL, napi_enumerable, NULL},

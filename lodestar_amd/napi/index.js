@@ -27,11 +27,41 @@ const path = require("path");
 
 // Every context's device batch runs on a libuv pool thread; contexts on
 // different devices run concurrently only if the pool has a thread for each
-// (default 4).  The pool is created on first use, so this must run before any
-// async work of the process (INTEGRATION.md section 4).
+// (default 4).  libuv reads UV_THREADPOOL_SIZE once, when the pool first
+// starts: in a host that has already done fs / crypto work (Lodestar has) this
+// default is ignored, so the launcher sets it before Node starts
+// (INTEGRATION.md section 4) and the constructor warns when it is too small.
 if (!process.env.UV_THREADPOOL_SIZE) process.env.UV_THREADPOOL_SIZE = "16";
 
 const addon = require(path.join(__dirname, "bgv.node"));
+
+// the library must be compiled from the sources beside it (tools/build.py
+// embeds their SHA-256 as bgv_build_id; lodestar_amd/native.py source_hash
+// is the same digest): a stale libbgv.so is refused instead of run
+function sourceHash(root = path.join(__dirname, "..", "..")) {
+  const fs = require("fs");
+  const crypto = require("crypto");
+  const csrc = path.join(root, "lodestar_amd", "csrc");
+  const files = fs.readdirSync(csrc).filter((f) => f.endsWith(".h") || f.endsWith(".hip")).sort()
+    .map((f) => "lodestar_amd/csrc/" + f).concat(["include/bgv.h"]);
+  const h = crypto.createHash("sha256");
+  for (const rel of files) {
+    const data = fs.readFileSync(path.join(root, rel));
+    const len = Buffer.alloc(8);
+    len.writeUInt32LE(data.length % 0x100000000, 0);
+    len.writeUInt32LE(Math.floor(data.length / 0x100000000), 4);
+    h.update(Buffer.concat([Buffer.from(rel + "\0"), len, data]));
+  }
+  return h.digest("hex");
+}
+
+function checkBuildId(id = addon.buildId()) {
+  const want = sourceHash();
+  if (id !== want && !id.startsWith(want + "+")) {
+    throw Error(`libbgv.so was built from other sources (id ${id.slice(0, 16)}, tree ${want.slice(0, 16)}): rebuild`);
+  }
+}
+checkBuildId();
 
 const MAX_SIGNATURE_SETS_PER_JOB = 128; // multithread/index.ts:39
 const MAX_BUFFERED_SIGS = 32; // multithread/index.ts:48
@@ -123,17 +153,31 @@ function encodeJobs(jobs) {
   return {jobOffsets, pkOffsets, pkIndices: Uint32Array.from(idx.length ? idx : [0]), msgs, sigs, sigLen, rawPks};
 }
 
-// whole jobs to `world` shards, greedy by set count (largest first), job
-// order kept inside a shard (lodestar_amd/dist.py shard_jobs)
-function shardJobs(sizes, world) {
+// device work of a job in Montgomery Fp products (lodestar_amd/dist.py
+// job_work, from tools/fpmul_counts.json): per set 13,790, per pubkey
+// reference 11 (one G1 mixed addition of the gather)
+const WORK_PER_SET = 13790;
+const WORK_PER_PUBKEY = 11;
+function jobWork(sets) {
+  let refs = 0;
+  for (const s of sets) refs += s.type === "single" ? 1 : s.pubkeys.length;
+  return sets.length * WORK_PER_SET + refs * WORK_PER_PUBKEY;
+}
+
+// whole jobs to `world` shards, greedy by work (largest first, each to the
+// least loaded shard), job order kept inside a shard (dist.py shard_jobs)
+function shardJobs(weights, world) {
   const shards = Array.from({length: world}, () => []);
   const load = new Array(world).fill(0);
-  const order = sizes.map((s, j) => j).sort((a, b) => sizes[b] - sizes[a] || a - b);
+  let floor = Infinity;
+  for (const w of weights) if (w > 0 && w < floor) floor = w;
+  if (floor === Infinity) floor = 1;
+  const order = weights.map((s, j) => j).sort((a, b) => weights[b] - weights[a] || a - b);
   for (const j of order) {
     let r = 0;
     for (let k = 1; k < world; k++) if (load[k] < load[r]) r = k;
     shards[r].push(j);
-    load[r] += Math.max(sizes[j], 1);
+    load[r] += Math.max(weights[j], floor);
   }
   return shards.map((s) => s.sort((a, b) => a - b));
 }
@@ -177,6 +221,14 @@ class BlsGpuVerifier {
   // holds a replica of the pubkey table
   constructor({device = 0, devices = null, maxSetsPerDeviceBatch = MAX_SETS_PER_DEVICE_BATCH, shardMinSets = SHARD_MIN_SETS} = {}) {
     const ids = devices && devices.length ? devices : [device];
+    // every device batch holds a libuv pool thread (napi_async_work); the pool
+    // size is read once, when the pool first starts, so the launcher must set
+    // UV_THREADPOOL_SIZE before Node runs any async work (INTEGRATION.md 4)
+    const pool = Number(process.env.UV_THREADPOOL_SIZE) || 4;
+    if (ids.length + 2 > pool) {
+      console.warn(`BlsGpuVerifier: ${ids.length} devices with UV_THREADPOOL_SIZE=${pool}: device batches will ` +
+        "serialise and starve other pool work; start Node with UV_THREADPOOL_SIZE >= devices + 2");
+    }
     this.ctxs = ids.map((d) => addon.open(d));
     this.ctx = this.ctxs[0];
     this.idle = ids.map(() => true);
@@ -259,10 +311,15 @@ class BlsGpuVerifier {
     this.jobs.push(...jobs);
   }
 
-  scheduleRun() {
+  // the first look comes a macro task later, as in the reference
+  // (setTimeout(runJob, 0), multithread/index.ts:242,299); the quiet-window
+  // re-looks use setImmediate, which Node does not clamp to 1 ms, so a lone
+  // block-import job pays microseconds for the coalescing, not milliseconds
+  scheduleRun(quiet = false) {
     if (!this.runScheduled) {
       this.runScheduled = true;
-      setTimeout(this.runJob, 0);
+      if (quiet) setImmediate(this.runJob);
+      else setTimeout(this.runJob, 0);
     }
   }
 
@@ -300,7 +357,7 @@ class BlsGpuVerifier {
         // jobs arrived since the last look: wait one more macro task
         this.seenSeq = this.pushSeq;
         this.quietWaits++;
-        this.scheduleRun();
+        this.scheduleRun(true);
         return;
       }
       this.quietWaits = 0;
@@ -344,13 +401,13 @@ class BlsGpuVerifier {
     this.scheduleRun();
   }
 
-  // SURVEY 8e: jobs sharded by set count over the devices, one partial Miller
+  // SURVEY 8e: jobs sharded by work (sets + pubkey references) over the devices, one partial Miller
   // product per shard (bgv_partial, concurrently on the libuv pool), ONE final
   // exponentiation of their product (bgv_combine_final); only when it fails
   // does each shard localise its failing jobs (bgv_partial_finish, the
   // worker's per-job retry).  Returns the result shape of addon.verify.
   async verifySharded(jobSets, devs) {
-    const shards = shardJobs(jobSets.map((s) => s.length), devs.length);
+    const shards = shardJobs(jobSets.map(jobWork), devs.length);
     const live = [];
     shards.forEach((ids, r) => ids.length && live.push({ctx: this.ctxs[devs[r]], ids}));
     if (live.length === 1) return addon.verify(live[0].ctx, encodeJobs(jobSets));
@@ -421,6 +478,6 @@ class BlsGpuVerifier {
 }
 
 module.exports = {
-  addon, BlsGpuVerifier, QueueError, chunkifyMaximizeChunkSize, encodeJobs, checkSets, shardJobs,
+  addon, BlsGpuVerifier, QueueError, sourceHash, checkBuildId, chunkifyMaximizeChunkSize, encodeJobs, checkSets, shardJobs, jobWork,
   MAX_BUFFERED_SIGS, MAX_BUFFER_WAIT_MS, MAX_JOBS_CAN_ACCEPT_WORK, SHARD_MIN_SETS,
 };

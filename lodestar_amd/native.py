@@ -46,7 +46,7 @@ PK_UNCOMPRESSED_96 = 1
 N_STAGES = 16
 
 EXPORTS = [
-    "bgv_abi_version", "bgv_set_code_name", "bgv_stage_name", "bgv_last_error", "bgv_open", "bgv_open_cfg",
+    "bgv_abi_version", "bgv_build_id", "bgv_set_code_name", "bgv_stage_name", "bgv_last_error", "bgv_open", "bgv_open_cfg",
     "bgv_cfg_default", "bgv_close",
     "bgv_pubkeys_set", "bgv_pubkeys_count", "bgv_pubkeys_get", "bgv_pubkeys_validate", "bgv_verify", "bgv_last_stats",
     "bgv_partial", "bgv_partial_finish", "bgv_combine_final", "bgv_debug_stages", "bgv_gen_keys", "bgv_gen_sign", "bgv_bench_fpmul",
@@ -142,9 +142,42 @@ class BgvDebug(ctypes.Structure):
 _lib = None
 _lib_lock = threading.Lock()
 
+ROOT = os.path.dirname(HERE)
+
+
+def source_files(root: str = ROOT) -> list[str]:
+    """The sources libbgv.so is compiled from, relative to the repo root."""
+    csrc = os.path.join(root, "lodestar_amd", "csrc")
+    names = sorted(f for f in os.listdir(csrc) if f.endswith((".h", ".hip")))
+    return [os.path.join("lodestar_amd", "csrc", f) for f in names] + [os.path.join("include", "bgv.h")]
+
+
+def source_hash(root: str = ROOT) -> str:
+    """SHA-256 over (path, content) of source_files(): the id tools/build.py
+    compiles into the library (bgv_build_id) and load_library checks."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for rel in source_files(root):
+        with open(os.path.join(root, rel), "rb") as f:
+            data = f.read()
+        h.update(rel.replace(os.sep, "/").encode() + b"\0" + len(data).to_bytes(8, "little") + data)
+    return h.hexdigest()
+
+
+def check_build_id(lib_id: str, root: str = ROOT) -> None:
+    """A library compiled from other sources than the tree beside it is
+    refused (variant builds carry the id plus '+' and their defines)."""
+    want = source_hash(root)
+    if lib_id != want and not lib_id.startswith(want + "+"):
+        raise BgvNativeError(BGV_E_INVALID_ARG,
+                             f"libbgv.so was built from other sources (id {lib_id[:16]}, tree {want[:16]}): "
+                             "rebuild with __graft_entry__.build()")
+
 
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load libbgv.so (no compute). Raises BgvNativeError when absent."""
+    """Load libbgv.so (no compute). Raises BgvNativeError when absent or when
+    it was not compiled from the sources in this tree."""
     global _lib
     with _lib_lock:
         if _lib is not None:
@@ -152,6 +185,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         if not os.path.exists(path):
             raise BgvNativeError(BGV_E_NO_DEVICE, f"{path} not built (run __graft_entry__.build())")
         lib = ctypes.CDLL(path)
+        lib.bgv_build_id.argtypes = []
+        lib.bgv_build_id.restype = ctypes.c_char_p
+        check_build_id(lib.bgv_build_id().decode())
         P = ctypes.c_void_p
         u32, i32, u64 = ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64
         sig = {

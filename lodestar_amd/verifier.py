@@ -44,7 +44,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import native
-from .dist import shard_jobs
+from .dist import job_work, shard_jobs
 
 MAX_SIGNATURE_SETS_PER_JOB = 128  # multithread/index.ts:39
 MAX_BUFFERED_SIGS = 32            # multithread/index.ts:48
@@ -474,14 +474,19 @@ class BlsGpuVerifier:
     def _run_device_batch(self, jobs: list[list[ISignatureSet]], devs: list[int] | None = None) -> list:
         """Verify a list of jobs on the devices `devs` (default: all); returns
         per job True / False / BlsError.  One device: bgv_verify.  Several: the
-        jobs are sharded by set count (dist.shard_jobs), every shard reduced to
+        jobs are sharded by work, sets + pubkey references (dist.job_work,
+        dist.shard_jobs), every shard reduced to
         a partial Miller product, the partials combined by one final
         exponentiation, and only when that fails each shard localised on its
         own device."""
         if not jobs:
             return []
         devs = list(range(len(self.devices))) if devs is None else list(devs)
-        shards = shard_jobs([len(j) for j in jobs], len(devs)) if len(devs) > 1 else [list(range(len(jobs)))]
+        if len(devs) > 1:
+            refs = [sum(1 if s.type == SignatureSetType.single else len(s.pubkeys) for s in j) for j in jobs]
+            shards = shard_jobs(job_work([len(j) for j in jobs], refs), len(devs))
+        else:
+            shards = [list(range(len(jobs)))]
         live = [(devs[r], ids) for r, ids in enumerate(shards) if ids]
         out: list = [None] * len(jobs)
         self.metrics["sets_started"] += sum(len(j) for j in jobs)

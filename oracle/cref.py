@@ -186,13 +186,17 @@ def bench_job_latency(w: _Workload, shape: list[int], reps: int = 5) -> dict:
 
 def bench_configs(threads: int, budget_s: float = 12.0, seed: int = 0x4C4F4445, table: int = 4096) -> dict:
     """CPU baseline for every BASELINE config with the reference pool's
-    semantics (multithread/index.ts:39,405-420): C1 (128 singles, one job,
+    semantics (multithread/index.ts:39,405-420): one set (verifyOnMainThread,
+    chain/validation/block.ts:146) and 3 / 8 / 32-set batches, C1 (128 singles, one job,
     BlsSingleThreadVerifier on one thread), C2 (64 x k=128 batchable gossip
     sets, one job on one worker), C3 (a block: 128 x k=128 + sync k=512 + 2
     singles, one job), C4 sets/s over `threads` workers, C5 = C4 with 1% of
     the sets faulted."""
     w = _Workload(threads, seed, table)
-    out = {"c1_singles_latency_ms": bench_job_latency(w, [1] * 128),
+    out = {"single_set_latency_ms": bench_job_latency(w, [1], reps=9),
+           # verifyMultipleSignatures of 3 / 8 / 32 sets (test/perf/bls/bls.test.ts:43-53)
+           "small_batch_latency_ms": {str(k): bench_job_latency(w, [1] * k)["p50"] for k in (3, 8, 32)},
+           "c1_singles_latency_ms": bench_job_latency(w, [1] * 128),
            "c2_gossip_latency_ms": bench_job_latency(w, [128] * 64),
            "c3_block_latency_ms": bench_job_latency(w, [128] * 128 + [512, 1, 1], reps=3)}
     out["c4"] = bench_segment_sample(budget_s=budget_s, threads=threads, work=w)

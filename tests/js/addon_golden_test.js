@@ -155,6 +155,18 @@ async function main() {
   assert.deepStrictEqual(blockRes.map((r, i) => r === (i !== 19)), new Array(32).fill(true));
   assert.ok(cs2Batches <= 2, `32 per-block calls took ${cs2Batches} device batches`);
   console.log(`range-sync pattern: 32 per-block calls -> ${cs2Batches} device batch(es)`);
+  // a lone non-batchable job (block import) is dispatched after the
+  // reference's one macro task (setTimeout 0, >= 1 ms) plus one unclamped
+  // setImmediate look for followers, not after extra 1-ms timer turns
+  const loneWaits = [];
+  for (let r = 0; r < 5; r++) {
+    const w1 = {...waits};
+    assert.strictEqual(await verifier.verifySignatureSets(sets), true);
+    loneWaits.push((waits.sum - w1.sum) * 1000);
+  }
+  loneWaits.sort((a, b) => a - b);
+  assert.ok(loneWaits[2] <= 3, `lone job waited ${loneWaits[2]} ms before dispatch (median of 5)`);
+  console.log(`lone non-batchable job: dispatch wait median ${loneWaits[2]} ms`);
 
   // 5. back-pressure: queued work joins the next batch, so canAcceptWork stays
   // true while a batch is in flight and turns false once a full next batch

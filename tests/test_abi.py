@@ -110,7 +110,8 @@ def test_cfg_defaults_and_validation(lib):
     assert {k: getattr(c, k) for k in native.BgvCfg.AUTO} == native.BgvCfg.AUTO
     h = ctypes.c_void_p()
     # invalid overrides are refused before any device call (no GPU needed)
-    for bad in ({"miller": 7}, {"job_lanes": 5}, {"pairs": 3}, {"defer_pct": 101}):
+    for bad in ({"miller": 7}, {"job_lanes": 5}, {"pairs": 3}, {"defer_pct": 101}, {"split": 2}, {"prefold": -2},
+                {"lines": 2}, {"timing": 5}, {"miller": 4, "pairs": 2}, {"miller": 36, "pairs": 2}):
         st = lib.bgv_open_cfg(0, ctypes.byref(native.BgvCfg.make(**bad)), ctypes.byref(h))
         assert st == native.BGV_E_INVALID_ARG, bad
     c2 = native.BgvCfg.make()
@@ -118,3 +119,40 @@ def test_cfg_defaults_and_validation(lib):
     assert lib.bgv_open_cfg(0, ctypes.byref(c2), ctypes.byref(h)) == native.BGV_E_INVALID_ARG
     with pytest.raises(ValueError):
         native.BgvCfg.make(overlap=0)
+
+
+def test_library_id_matches_the_sources(lib):
+    """tools/build.py compiles the SHA-256 of csrc/ + include/bgv.h into the
+    library; load_library refuses a library built from other sources."""
+    from lodestar_amd import native
+    assert lib.bgv_build_id().decode() == native.source_hash()
+
+
+def test_stale_library_refuses_to_load(lib, tmp_path):
+    import shutil
+
+    from lodestar_amd import native
+    lib_id = lib.bgv_build_id().decode()
+    # a tree whose sources differ from the ones the library was built from
+    for rel in native.source_files():
+        dst = tmp_path / rel
+        dst.parent.mkdir(parents=True, exist_ok=True)
+        shutil.copy(os.path.join(ROOT, rel), dst)
+    native.check_build_id(lib_id, root=str(tmp_path))  # same sources: accepted
+    fp = tmp_path / "lodestar_amd" / "csrc" / "fp.h"
+    fp.write_text(fp.read_text() + "\n// edited\n")
+    with pytest.raises(native.BgvNativeError, match="other sources"):
+        native.check_build_id(lib_id, root=str(tmp_path))
+    # and in a fresh interpreter the stale tree's library does not load at all
+    shutil.copytree(os.path.join(ROOT, "lodestar_amd"), tmp_path / "pkg" / "lodestar_amd",
+                    ignore=shutil.ignore_patterns("__pycache__", "napi"))
+    (tmp_path / "pkg" / "include").mkdir()
+    shutil.copy(HEADER, tmp_path / "pkg" / "include" / "bgv.h")
+    hdr = tmp_path / "pkg" / "lodestar_amd" / "csrc" / "fp.h"
+    hdr.write_text(hdr.read_text() + "\n// edited\n")
+    code = ("import sys; sys.path.insert(0, %r)\nfrom lodestar_amd import native\n"
+            "try:\n    native.load_library()\nexcept native.BgvNativeError as e:\n    print('refused', e)\n") % str(tmp_path / "pkg")
+    env = dict(os.environ)
+    env.pop("BGV_LIB", None)
+    out = subprocess.check_output([__import__("sys").executable, "-c", code], env=env).decode()
+    assert out.startswith("refused") and "other sources" in out

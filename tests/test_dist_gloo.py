@@ -49,15 +49,22 @@ class FakeShardDevice:
         return self._t.copy()
 
 
+# ten blocks: sets and pubkey references (with and without the 512-key sync
+# aggregate, one near-empty block); shards are balanced by dist.job_work
+JOB_SETS = [98, 98, 97, 98, 97, 98, 98, 97, 98, 2]
+JOB_REFS = [95 * 128 + 514, 95 * 128 + 514, 95 * 128 + 2, 95 * 128 + 514, 95 * 64 + 2, 95 * 128 + 514,
+            95 * 160 + 514, 95 * 128 + 2, 95 * 128 + 514, 2]
+
+
 def _worker(rank, world, port, q, truth):
     import torch.distributed as dist
-    from lodestar_amd.dist import allgather_partials, gather_job_results, shard_jobs, verify_sharded
+    from lodestar_amd.dist import allgather_partials, gather_job_results, job_work, shard_jobs, verify_sharded
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     part = bytes([rank + 1]) * 576
     parts = allgather_partials(part, dist)
-    shards = shard_jobs([98] * 9 + [40], world)
+    shards = shard_jobs(job_work(JOB_SETS, JOB_REFS), world)
     out = {"firsts": [p[0] for p in parts], "lens": [len(p) for p in parts], "shard": shards[rank]}
     for name, t in truth.items():
         dev = FakeShardDevice(t)
@@ -96,6 +103,10 @@ def test_sharded_verdicts_gloo_world2():
             assert valid == want_valid
             assert finished == (0 if want_valid else 1)  # localisation only after a failed combined check
     assert sorted(res[0]["shard"] + res[1]["shard"]) == list(range(10))
+    from lodestar_amd.dist import job_work
+    w = job_work(JOB_SETS, JOB_REFS)
+    loads = [sum(w[j] for j in res[r]["shard"]) for r in range(world)]
+    assert max(loads) - min(loads) <= max(w)  # whole jobs: at most one job apart
 
 
 def test_select_jobs_rebases_offsets():

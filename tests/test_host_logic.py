@@ -1,12 +1,15 @@
 """Host logic of the IBlsVerifier mirror (no GPU): chunking, batch encoding,
 error strings, block-level verdict ordering and job sharding."""
 import asyncio
+import os
 
 import numpy as np
 import pytest
 
 from lodestar_amd import verifier as V
-from lodestar_amd.dist import shard_jobs
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+from lodestar_amd.dist import batch_job_work, job_work, shard_balance, shard_jobs
 
 
 def test_chunkify_matches_reference_unit_test():
@@ -90,3 +93,62 @@ def test_shard_jobs_balanced_and_complete():
         assert flat == list(range(len(sizes)))
         loads = [sum(sizes[j] for j in s) for s in shards]
         assert max(loads) - min(loads) <= 128
+
+
+def mixed_segment_jobs(n_blocks=256, seed=7):
+    """(sets, pubkey refs) per block of a mixed range-sync segment: full blocks
+    with the 512-key sync aggregate, full blocks without it, blocks of fewer
+    and smaller attestations, and near-empty blocks (proposer + randao)"""
+    import random
+    rnd = random.Random(seed)
+    out = []
+    for _ in range(n_blocks):
+        kind = rnd.random()
+        if kind < 0.1:  # near-empty: proposer + randao
+            out.append((2, 2))
+        else:
+            n_att = rnd.randint(8, 95) if kind < 0.35 else 95
+            k = [rnd.choice((64, 96, 128, 160)) for _ in range(n_att)]
+            sync = kind < 0.7  # with or without the sync aggregate
+            out.append((n_att + 2 + sync, sum(k) + 2 + 512 * sync))
+    return out
+
+
+def test_shard_jobs_balance_work_on_a_mixed_segment():
+    """shards balanced by sum W(k) (sets + pubkey references), not
+    by set count; within 5% max/mean over 8 shards on a mixed segment"""
+    jobs = mixed_segment_jobs()
+    work = job_work([s for s, _ in jobs], [k for _, k in jobs])
+    for world in (2, 4, 8):
+        shards = shard_jobs(work, world)
+        assert sorted(j for s in shards for j in s) == list(range(len(jobs)))
+        assert shard_balance(work, shards) <= 1.05, world
+    # a 512-key sync job outweighs a 1-key single, so they no longer count the same
+    a, b = job_work([1, 1], [512, 1])
+    assert a > b
+
+
+def test_batch_job_work_matches_job_work():
+    jo = np.array([0, 2, 5, 5, 6], np.uint32)
+    po = np.array([0, 1, 513, 641, 642, 643, 771], np.uint32)
+    assert batch_job_work({"job_offsets": jo, "pk_offsets": po}) == job_work([2, 3, 0, 1], [513, 130, 0, 128])
+
+
+def test_node_shard_jobs_is_the_python_assignment():
+    import json
+    import shutil
+    import subprocess
+    from tools import build
+    if not shutil.which("node") or not build.build_addon():
+        pytest.skip("node or its headers are absent")
+    jobs = mixed_segment_jobs(64, seed=3)
+    sets = [[{"type": "aggregate", "pubkeys": [0] * (k // s)} for _ in range(s)] for s, k in jobs]
+    # give every job exactly k references: the first set takes the remainder
+    for (s, k), js in zip(jobs, sets):
+        js[0]["pubkeys"] = [0] * (k - (k // s) * (s - 1))
+    script = ("const m = require(%r); const jobs = JSON.parse(require('fs').readFileSync(0, 'utf8'));"
+              "console.log(JSON.stringify([8, 4, 2].map((w) => m.shardJobs(jobs.map(m.jobWork), w))));") % os.path.join(
+                  ROOT, "lodestar_amd", "napi", "index.js")
+    out = json.loads(subprocess.check_output(["node", "-e", script], input=json.dumps(sets).encode()))
+    work = job_work([s for s, _ in jobs], [k for _, k in jobs])
+    assert out == [shard_jobs(work, w) for w in (8, 4, 2)]
