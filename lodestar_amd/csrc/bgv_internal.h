@@ -135,6 +135,7 @@ void launch_sig_split_coop(hipStream_t st, const dev_batch& b, const dev_work& w
 void launch_hash_clear_coop(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_latency.hip
 void launch_hash_clear_trio(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_latency.hip
 void launch_s_level_coop(hipStream_t st, const dev_batch& b, const dev_work& w, uint32_t s);  // bgv_latency.hip
+void launch_msm_job_coop(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_latency.hip
 void launch_fp12_tail(hipStream_t st, int stage, const dev_batch& b, const dev_work& w);  // bgv_tail.hip
 void launch_combine_final(hipStream_t st, const fp12_t* parts, uint32_t n, uint32_t* flag);
 void launch_final_exp_many(hipStream_t st, const fp12_t* in, fp12_t* out, uint32_t n);  // bgv_debug_stages

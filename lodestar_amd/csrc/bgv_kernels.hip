@@ -315,6 +315,12 @@ __global__ void BGV_BULK k_job_recode(dev_batch b, dev_work w) {
 #ifndef BGV_COOP_G2
 #define BGV_COOP_G2 1
 #endif
+#ifndef BGV_MSM_JOB_COOP
+#define BGV_MSM_JOB_COOP 1
+#endif
+#ifndef BGV_MSM_JOB_COOP_BULK
+#define BGV_MSM_JOB_COOP_BULK 0
+#endif
 
 // latency mode: lane t maps u_(t & 1) of message t >> 1; then one lane per
 // message adds the two points and clears the cofactor
@@ -1213,7 +1219,12 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       BGV_LAUNCH(k_set_job, b.n_jobs, b, w);
       if (b.msm == 2 || b.msm == 4) {
         if (b.msm == 2) BGV_LAUNCH(k_msm_window, b.n_jobs * 16u, b, w);
-        BGV_LAUNCH(k_msm_job, b.n_jobs * 16u, b, w);
+        // the window combination on nine lanes per job (bgv_latency.hip) in
+        // the latency mode; bulk batches keep the 16-lane one-lane form
+        if ((b.msm == 4 && BGV_MSM_JOB_COOP) || (b.msm == 2 && BGV_MSM_JOB_COOP_BULK))
+          launch_msm_job_coop(st, b, w);
+        else
+          BGV_LAUNCH(k_msm_job, b.n_jobs * 16u, b, w);
         break;
       }
       if (b.msm == 1) {

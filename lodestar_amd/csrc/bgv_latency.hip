@@ -116,6 +116,49 @@ __global__ void __launch_bounds__(64, 1) k_s_level_coop(dev_batch b, dev_work w,
   if (own && sl == 0 && q == 0) w.rsig[i] = r;
 }
 
+// per job: S_job = sum_w 16^w S_w from the MSM's 16 window sums (msm_win,
+// k_msm_digit / k_msm_window) by Horner on nine lanes per job (seven jobs per
+// wave): 60 cooperative doublings (3 rounds of one Fp product each) and 15
+// additions, against the one-lane form's 60 doublings of ~16 sequential Fp
+// products each (bgv_kernels.hip k_msm_job: 2.8 ms at 12,544 sets).  Codes as
+// k_job_s (first failing set code, signatures before pubkeys).  S_job's affine
+// value does not depend on the order of the additions.
+__global__ void __launch_bounds__(64, 1) k_msm_job_coop(dev_batch b, dev_work w) {
+  __shared__ cg_scratch sm[CG_GROUPS + 1];
+  const uint32_t lane = threadIdx.x, grp = lane / CG_LANES, r9 = lane % CG_LANES, sl = r9 / 3, q = r9 % 3;
+  const uint32_t j0 = blockIdx.x * CG_GROUPS + grp;
+  const bool own = grp < CG_GROUPS && j0 < b.n_jobs;
+  const uint32_t j = own ? j0 : 0u;
+  const uint32_t beg = b.job_off[j], end = b.job_off[j + 1];
+  int32_t code = C_OK;
+  for (uint32_t i = beg; i < end && code == C_OK; i++) code = w.sig_code[i];
+  for (uint32_t i = beg; i < end && code == C_OK; i++) code = w.pk_code[i];
+  if (end == beg) code = C_EMPTY_JOB;
+  const g2j* win = w.msm_win + 16u * j;
+  g2j s = win[15];
+#pragma unroll 1
+  for (int k = 14; k >= 0; k--) {
+    cg_dbl<3>(&sm[grp], sl, q, s, s);
+    cg_dbl<3>(&sm[grp], sl, q, s, s);
+    cg_dbl<3>(&sm[grp], sl, q, s, s);
+    cg_dbl<3>(&sm[grp], sl, q, s, s);
+    cg_add<3>(&sm[grp], sl, q, s, s, win[k]);
+  }
+  if (!own || sl != 0 || q != 0) return;
+  g2a sa;
+  sa.x = fp2_zero();
+  sa.y = fp2_zero();
+  uint32_t inf = 1;
+  if (code == C_OK) inf = jac_to_aff(sa, s) ? 0u : 1u;
+  w.s_aff[j] = sa;
+  w.s_inf[j] = inf;
+  w.job_code[j] = code;
+}
+
+void launch_msm_job_coop(hipStream_t st, const dev_batch& b, const dev_work& w) {
+  if (b.n_jobs) hipLaunchKernelGGL(k_msm_job_coop, dim3((b.n_jobs + CG_GROUPS - 1) / CG_GROUPS), dim3(64), 0, st, b, w);
+}
+
 void launch_s_level_coop(hipStream_t st, const dev_batch& b, const dev_work& w, uint32_t s) {
   if (b.n_sets) hipLaunchKernelGGL(k_s_level_coop, dim3((b.n_sets + CG_GROUPS - 1) / CG_GROUPS), dim3(64), 0, st, b, w, s);
 }

@@ -23,6 +23,9 @@ constexpr int CG_GROUPS = 64 / CG_LANES;  // 7 points per wave
 #ifndef BGV_CG_SPLIT_COMBINE
 #define BGV_CG_SPLIT_COMBINE 1
 #endif
+#ifndef BGV_CG_TRIO_BATCH
+#define BGV_CG_TRIO_BATCH 1
+#endif
 
 // force-inline the round and the point steps into the latency kernels (A/B knob)
 #ifndef BGV_CG_INLINE
@@ -84,9 +87,48 @@ BGV_CGF void cg_round(cg_scratch* S, uint32_t s, uint32_t q, int n, const fp2_t&
                          const fp2_t& a1, const fp2_t& b1, const fp2_t& a2, const fp2_t& b2, fp2_t& o0, fp2_t& o1,
                          fp2_t& o2) {
   if constexpr (SLOTS == 1) {
+#if BGV_CG_TRIO_BATCH
+    // three lanes: lane q forms Karatsuba sub-product q of EVERY Fp2 product
+    // of the round (n Fp products in a row), then ONE exchange and every lane
+    // combines the n products: n product latencies + 1 exchange, against n x
+    // (1 product + 1 exchange) when the products go through one at a time
+    BGV_LDS cg_scratch* L = (BGV_LDS cg_scratch*)S;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      if (k >= n) break;
+      const fp2_t& a = k == 0 ? a0 : (k == 1 ? a1 : a2);
+      const fp2_t& b = k == 0 ? b0 : (k == 1 ? b1 : b2);
+      fp_t u, v;
+      if (q == 0) {
+        u = a.c0;
+        v = b.c0;
+      } else if (q == 1) {
+        u = a.c1;
+        v = b.c1;
+      } else {
+        fp_add_lazy(u, a.c0, a.c1);  // < 2p, product inputs only
+        fp_add_lazy(v, b.c0, b.c1);
+      }
+      fp_t r;
+      fp_mul(r, u, v);
+      lds_put(&L->P[k][q], r);
+    }
+    coop_wave_sync();
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      if (k >= n) break;
+      fp2_t& o = k == 0 ? o0 : (k == 1 ? o1 : o2);
+      const fp_t p0 = lds_get(&L->P[k][0]), p1 = lds_get(&L->P[k][1]), p2 = lds_get(&L->P[k][2]);
+      fp_t w;
+      fp_add_sub(w, p0, p1, o.c0, p0, p1);
+      fp_sub(o.c1, p2, w);
+    }
+    coop_wave_sync();
+#else
     cg_prod1(S, q, a0, b0, o0);
     if (n > 1) cg_prod1(S, q, a1, b1, o1);
     if (n > 2) cg_prod1(S, q, a2, b2, o2);
+#endif
     return;
   }
   const fp2_t a = cg_sel(s, a0, a1, a2), b = cg_sel(s, b0, b1, b2);
