@@ -24,6 +24,14 @@
 #endif
 #include "bgv_internal.h"
 #include "coop_g2.h"
+#include "kv_g2.h"
+
+#ifndef BGV_KV_CLEAR
+#define BGV_KV_CLEAR 1  // three-lane clearing in views (kv_g2.h)
+#endif
+#ifndef BGV_KV9
+#define BGV_KV9 1  // nine-lane G2 kernels in views (kv_g2.h)
+#endif
 
 namespace bgv {
 
@@ -91,8 +99,95 @@ __global__ void __launch_bounds__(64, 1) k_hash_clear_trio(dev_batch b, dev_work
   }
 }
 
+// The same clearing in Karatsuba views (kv_g2.h): each lane of the three
+// holds one Fp view of every Fp2 value, so the point formulas' additions are
+// one Fp operation per lane and no operand is selected before a product
+constexpr int KV1_GROUPS = 21;
+__global__ void __launch_bounds__(64, 1) k_hash_clear_kv(dev_batch b, dev_work w) {
+  __shared__ kv_scratch<1> sm[KV1_GROUPS + 1];
+  const uint32_t lane = threadIdx.x, grp = lane / 3u, q = lane % 3u;
+  const uint32_t i0 = blockIdx.x * KV1_GROUPS + grp;
+  const bool own = grp < (uint32_t)KV1_GROUPS && i0 < b.n_sets;
+  const uint32_t i = own ? i0 : 0u;
+  const kv_grp<1> g{&sm[grp], grp, 0u, q};
+  kv_init<1>(g.sc, 0u, q);
+  kv_pt p0, p1, r, h;
+  kv_load(p0, w.q_part[2u * i], q);
+  kv_load(p1, w.q_part[2u * i + 1u], q);
+  kv_add<1>(g, r, p0, p1);
+  kv_clear_cofactor<1>(g, h, r);
+  g2j hj;
+  kv_gather<1>(g, hj, h);
+  if (own && q == 0) {
+    g2a ha;
+    jac_to_aff(ha, hj);
+    w.h_aff[i] = ha;
+  }
+}
+
+// nine lanes per point in views (three slots x three views): the layouts of
+// k_hash_clear_coop / k_sig_split_coop / k_s_level_coop / k_msm_job_coop
+// with kv_g2.h arithmetic
+constexpr int KV3_GROUPS = 7;
+__global__ void __launch_bounds__(64, 1) k_hash_clear_kv9(dev_batch b, dev_work w) {
+  __shared__ kv_scratch<3> sm[KV3_GROUPS + 1];
+  const uint32_t lane = threadIdx.x, grp = lane / 9u, r9 = lane % 9u, s = r9 / 3u, q = r9 % 3u;
+  const uint32_t i0 = blockIdx.x * KV3_GROUPS + grp;
+  const bool own = grp < (uint32_t)KV3_GROUPS && i0 < b.n_sets;
+  const uint32_t i = own ? i0 : 0u;
+  const kv_grp<3> g{&sm[grp], grp, s, q};
+  kv_init<3>(g.sc, s, q);
+  kv_pt p0, p1, r, h;
+  kv_load(p0, w.q_part[2u * i], q);
+  kv_load(p1, w.q_part[2u * i + 1u], q);
+  kv_add<3>(g, r, p0, p1);
+  kv_clear_cofactor<3>(g, h, r);
+  g2j hj;
+  kv_gather<3>(g, hj, h);
+  if (own && s == 0 && q == 0) {
+    g2a ha;
+    jac_to_aff(ha, hj);
+    w.h_aff[i] = ha;
+  }
+}
+
+__global__ void __launch_bounds__(64, 1) k_sig_split_kv9(dev_batch b, dev_work w) {
+  __shared__ kv_scratch<3> sm[KV3_GROUPS + 1];
+  __shared__ g2j tabs[KV3_GROUPS][16];
+  const uint32_t nbg = (b.n_sets + KV3_GROUPS - 1) / KV3_GROUPS;
+  const bool check = blockIdx.x < nbg;
+  const uint32_t lane = threadIdx.x, grp = lane / 9u, r9 = lane % 9u, s = r9 / 3u, q = r9 % 3u;
+  const uint32_t i0 = (check ? blockIdx.x : blockIdx.x - nbg) * KV3_GROUPS + grp;
+  const bool own = grp < (uint32_t)KV3_GROUPS && i0 < b.n_sets;
+  const uint32_t i = own ? i0 : 0u;
+  const bool lead = own && s == 0 && q == 0;
+  const bool live = w.sig_code[i] == C_OK && !w.sig_inf[i];  // decode outcome (k_sig_dec)
+  const kv_grp<3> g{&sm[grp], grp, s, q};
+  kv_init<3>(g.sc, s, q);
+  g2j pj;
+  jac_from_aff(pj, w.sig_aff[i]);
+  kv_pt p;
+  kv_load(p, pj, q);
+  if (check) {
+    const bool ok = kv_in_subgroup<3>(g, p);
+    if (lead) w.sig_grp[i] = (!live || ok) ? 1u : 0u;
+  } else {
+    kv_pt r;
+    // lane 63 (grp 7) computes on group 6's table without writing it
+    kv_mul_u64_w4<3>(g, tabs[grp < (uint32_t)KV3_GROUPS ? grp : KV3_GROUPS - 1u], grp < (uint32_t)KV3_GROUPS, r, p, b.scalars[i]);
+    g2j rj;
+    kv_gather<3>(g, rj, r);
+    if (!live) jac_set_inf(rj);  // infinity signature: blst skips it (adds the identity)
+    if (lead) w.rsig[i] = rj;
+  }
+}
+
 void launch_hash_clear_trio(hipStream_t st, const dev_batch& b, const dev_work& w) {
-  if (b.n_sets) hipLaunchKernelGGL(k_hash_clear_trio, dim3((b.n_sets + CG3_GROUPS - 1) / CG3_GROUPS), dim3(64), 0, st, b, w);
+  if (!b.n_sets) return;
+  if (BGV_KV_CLEAR)
+    hipLaunchKernelGGL(k_hash_clear_kv, dim3((b.n_sets + KV1_GROUPS - 1) / KV1_GROUPS), dim3(64), 0, st, b, w);
+  else
+    hipLaunchKernelGGL(k_hash_clear_trio, dim3((b.n_sets + CG3_GROUPS - 1) / CG3_GROUPS), dim3(64), 0, st, b, w);
 }
 
 // One level of the per-job signature sum (bgv_kernels.hip k_s_level) on nine
@@ -116,6 +211,28 @@ __global__ void __launch_bounds__(64, 1) k_s_level_coop(dev_batch b, dev_work w,
   if (own && sl == 0 && q == 0) w.rsig[i] = r;
 }
 
+__global__ void __launch_bounds__(64, 1) k_s_level_kv9(dev_batch b, dev_work w, uint32_t s) {
+  __shared__ kv_scratch<3> sm[KV3_GROUPS + 1];
+  const uint32_t lane = threadIdx.x, grp = lane / 9u, r9 = lane % 9u, sl = r9 / 3u, q = r9 % 3u;
+  const uint32_t i0 = blockIdx.x * KV3_GROUPS + grp;
+  bool own = grp < (uint32_t)KV3_GROUPS && i0 < b.n_sets;
+  if (own) {
+    const uint32_t j = w.set_job[i0];
+    own = ((i0 - b.job_off[j]) % (2u * s)) == 0 && i0 + s < b.job_off[j + 1];
+  }
+  if (!__any(own)) return;  // wave-uniform
+  const uint32_t i = own ? i0 : 0u, k = own ? i0 + s : 0u;
+  const kv_grp<3> g{&sm[grp], grp, sl, q};
+  kv_init<3>(g.sc, sl, q);
+  kv_pt a, c, r;
+  kv_load(a, w.rsig[i], q);
+  kv_load(c, w.rsig[k], q);
+  kv_add<3>(g, r, a, c);
+  g2j rj;
+  kv_gather<3>(g, rj, r);
+  if (own && sl == 0 && q == 0) w.rsig[i] = rj;
+}
+
 // per job: S_job = sum_w 16^w S_w from the MSM's 16 window sums (msm_win,
 // k_msm_digit / k_msm_window) by Horner on nine lanes per job (seven jobs per
 // wave): 60 cooperative doublings (3 rounds of one Fp product each) and 15
@@ -124,7 +241,11 @@ __global__ void __launch_bounds__(64, 1) k_s_level_coop(dev_batch b, dev_work w,
 // k_job_s (first failing set code, signatures before pubkeys).  S_job's affine
 // value does not depend on the order of the additions.
 __global__ void __launch_bounds__(64, 1) k_msm_job_coop(dev_batch b, dev_work w) {
+  #if BGV_KV9
+  __shared__ kv_scratch<3> smk[KV3_GROUPS + 1];
+#else
   __shared__ cg_scratch sm[CG_GROUPS + 1];
+#endif
   const uint32_t lane = threadIdx.x, grp = lane / CG_LANES, r9 = lane % CG_LANES, sl = r9 / 3, q = r9 % 3;
   const uint32_t j0 = blockIdx.x * CG_GROUPS + grp;
   const bool own = grp < CG_GROUPS && j0 < b.n_jobs;
@@ -135,7 +256,26 @@ __global__ void __launch_bounds__(64, 1) k_msm_job_coop(dev_batch b, dev_work w)
   for (uint32_t i = beg; i < end && code == C_OK; i++) code = w.pk_code[i];
   if (end == beg) code = C_EMPTY_JOB;
   const g2j* win = w.msm_win + 16u * j;
-  g2j s = win[15];
+  g2j s;
+#if BGV_KV9
+  {
+    const kv_grp<3> g{&smk[grp], grp, sl, q};
+    kv_init<3>(g.sc, sl, q);
+    kv_pt acc, e;
+    kv_load(acc, win[15], q);
+#pragma unroll 1
+    for (int k = 14; k >= 0; k--) {
+      kv_dbl<3>(g, acc, acc);
+      kv_dbl<3>(g, acc, acc);
+      kv_dbl<3>(g, acc, acc);
+      kv_dbl<3>(g, acc, acc);
+      kv_load(e, win[k], q);
+      kv_add<3>(g, acc, acc, e);
+    }
+    kv_gather<3>(g, s, acc);
+  }
+#else
+  s = win[15];
 #pragma unroll 1
   for (int k = 14; k >= 0; k--) {
     cg_dbl<3>(&sm[grp], sl, q, s, s);
@@ -144,6 +284,7 @@ __global__ void __launch_bounds__(64, 1) k_msm_job_coop(dev_batch b, dev_work w)
     cg_dbl<3>(&sm[grp], sl, q, s, s);
     cg_add<3>(&sm[grp], sl, q, s, s, win[k]);
   }
+#endif
   if (!own || sl != 0 || q != 0) return;
   g2a sa;
   sa.x = fp2_zero();
@@ -160,15 +301,23 @@ void launch_msm_job_coop(hipStream_t st, const dev_batch& b, const dev_work& w) 
 }
 
 void launch_s_level_coop(hipStream_t st, const dev_batch& b, const dev_work& w, uint32_t s) {
-  if (b.n_sets) hipLaunchKernelGGL(k_s_level_coop, dim3((b.n_sets + CG_GROUPS - 1) / CG_GROUPS), dim3(64), 0, st, b, w, s);
+  if (!b.n_sets) return;
+  if (BGV_KV9) hipLaunchKernelGGL(k_s_level_kv9, dim3((b.n_sets + KV3_GROUPS - 1) / KV3_GROUPS), dim3(64), 0, st, b, w, s);
+  else hipLaunchKernelGGL(k_s_level_coop, dim3((b.n_sets + CG_GROUPS - 1) / CG_GROUPS), dim3(64), 0, st, b, w, s);
 }
 
 void launch_sig_split_coop(hipStream_t st, const dev_batch& b, const dev_work& w) {
-  if (b.n_sets) hipLaunchKernelGGL(k_sig_split_coop, dim3(2u * ((b.n_sets + CG_GROUPS - 1) / CG_GROUPS)), dim3(64), 0, st, b, w);
+  if (!b.n_sets) return;
+  if (BGV_KV9)
+    hipLaunchKernelGGL(k_sig_split_kv9, dim3(2u * ((b.n_sets + KV3_GROUPS - 1) / KV3_GROUPS)), dim3(64), 0, st, b, w);
+  else
+    hipLaunchKernelGGL(k_sig_split_coop, dim3(2u * ((b.n_sets + CG_GROUPS - 1) / CG_GROUPS)), dim3(64), 0, st, b, w);
 }
 
 void launch_hash_clear_coop(hipStream_t st, const dev_batch& b, const dev_work& w) {
-  if (b.n_sets) hipLaunchKernelGGL(k_hash_clear_coop, dim3((b.n_sets + CG_GROUPS - 1) / CG_GROUPS), dim3(64), 0, st, b, w);
+  if (!b.n_sets) return;
+  if (BGV_KV9) hipLaunchKernelGGL(k_hash_clear_kv9, dim3((b.n_sets + KV3_GROUPS - 1) / KV3_GROUPS), dim3(64), 0, st, b, w);
+  else hipLaunchKernelGGL(k_hash_clear_coop, dim3((b.n_sets + CG_GROUPS - 1) / CG_GROUPS), dim3(64), 0, st, b, w);
 }
 
 }  // namespace bgv

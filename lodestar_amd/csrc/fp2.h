@@ -61,6 +61,28 @@ BGV_HD void fp_add_lazy2(fp_t& r0, const fp_t& a0, const fp_t& b0, fp_t& r1, con
 #endif
 }
 
+// three independent modular additions / subtractions (one asm block)
+BGV_HD void fp_add3(fp_t& r0, const fp_t& a0, const fp_t& b0, fp_t& r1, const fp_t& a1, const fp_t& b1, fp_t& r2,
+                    const fp_t& a2, const fp_t& b2) {
+#if BGV_ASM_ON
+  fpa_add_add_add(r0, a0, b0, r1, a1, b1, r2, a2, b2);
+#else
+  fp_add(r0, a0, b0);
+  fp_add(r1, a1, b1);
+  fp_add(r2, a2, b2);
+#endif
+}
+BGV_HD void fp_sub3(fp_t& r0, const fp_t& a0, const fp_t& b0, fp_t& r1, const fp_t& a1, const fp_t& b1, fp_t& r2,
+                    const fp_t& a2, const fp_t& b2) {
+#if BGV_ASM_ON
+  fpa_sub_sub_sub(r0, a0, b0, r1, a1, b1, r2, a2, b2);
+#else
+  fp_sub(r0, a0, b0);
+  fp_sub(r1, a1, b1);
+  fp_sub(r2, a2, b2);
+#endif
+}
+
 BGV_HD void fp2_add(fp2_t& r, const fp2_t& a, const fp2_t& b) { fp_add2(r.c0, a.c0, b.c0, r.c1, a.c1, b.c1); }
 BGV_HD void fp2_sub(fp2_t& r, const fp2_t& a, const fp2_t& b) { fp_sub2(r.c0, a.c0, b.c0, r.c1, a.c1, b.c1); }
 BGV_HD void fp2_dbl(fp2_t& r, const fp2_t& a) { fp_add2(r.c0, a.c0, a.c0, r.c1, a.c1, a.c1); }
