@@ -148,6 +148,7 @@ typedef struct bgv_stats {
   uint32_t lines;               /* 1: fixed-argument Miller lines */
   uint32_t defer_from;          /* subgroup checks of sets >= defer_from run beside the Miller loops (n_sets: none) */
   uint32_t clear_lanes;         /* latency mode: lanes per point of the cofactor clearing */
+  uint32_t miller_kv;           /* 0, or the product slots of the two-pair Miller loop in Karatsuba views (3 S lanes per two pairs) */
 } bgv_stats;
 
 /* Pipeline overrides for tests and A/B tools.  Production opens contexts with
@@ -166,6 +167,7 @@ typedef struct bgv_cfg {
   int32_t defer_pct;    /* -1 auto; 0..100: share of the G2 subgroup checks run beside the Miller loops (bulk mode) */
   int32_t timing;       /* -1 auto (batches >= 65,536 sets); 0 / 1 per-stage timing events */
   int32_t clear_lanes;  /* -1 auto; 1 / 3 / 9 lanes per point of the latency mode's cofactor clearing */
+  int32_t miller_kv;    /* -1 auto; 0 off; 3 / 6: the two-pair Miller loop in Karatsuba views on 9 / 18 lanes per two pairs */
 } bgv_cfg;
 /* every field "auto" */
 void bgv_cfg_default(bgv_cfg* cfg);

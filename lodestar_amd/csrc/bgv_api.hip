@@ -165,6 +165,7 @@ void bgv_cfg_default(bgv_cfg* cfg) {
   memset(cfg, 0, sizeof *cfg);
   cfg->struct_size = sizeof *cfg;
   cfg->split = cfg->miller = cfg->msm = cfg->prefold = cfg->lines = cfg->defer_pct = cfg->timing = cfg->clear_lanes = -1;
+  cfg->miller_kv = -1;
   cfg->job_lanes = cfg->pairs = 0;
 }
 
@@ -185,6 +186,8 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
     if (k.msm < -1 || k.msm > 4) return fail(BGV_E_INVALID_ARG, "bgv_cfg.msm %d", k.msm);
     if (k.clear_lanes != -1 && k.clear_lanes != 1 && k.clear_lanes != 3 && k.clear_lanes != 9)
       return fail(BGV_E_INVALID_ARG, "bgv_cfg.clear_lanes %d", k.clear_lanes);
+    if (k.miller_kv != -1 && k.miller_kv != 0 && k.miller_kv != 3 && k.miller_kv != 6)
+      return fail(BGV_E_INVALID_ARG, "bgv_cfg.miller_kv %d", k.miller_kv);
     if (k.defer_pct < -1 || k.defer_pct > 100) return fail(BGV_E_INVALID_ARG, "bgv_cfg.defer_pct %d", k.defer_pct);
     auto tri_ok = [](int v) { return v >= -1 && v <= 1; };
     if (!tri_ok(k.split)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.split %d", k.split);
@@ -548,6 +551,14 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   d.miller_coop = k.miller >= 0 ? (k.miller == 1 ? 0u : (uint32_t)k.miller)
                                 : (n < MILLER18_MIN ? 36u : n < MILLER4_MIN ? 18u : n < MILLER2_MIN ? 4u
                                    : n < MILLER1_MIN ? 2u : 0u);
+  // two-pair Miller loop in Karatsuba views (miller_kv.h) in the latency mode:
+  // the squaring of f is shared by two pairs, 3 S lanes per two pairs
+  {
+    const uint32_t auto_kv = 0u;
+    d.miller_kv = k.miller_kv >= 0 ? (uint32_t)k.miller_kv : auto_kv;
+    if (!d.split) d.miller_kv = 0;
+    if (d.miller_kv) d.pairs_per_item = 2;
+  }
   // fixed-argument lines (pairing.h miller_lines): the G2 half of the one-lane
   // Miller loop moves to the hash stream, phase 1 (C4 40.4 -> 39.5 ms); with
   // one pair per item it loses (C4/2 26.4 -> 28.5 ms)
@@ -737,6 +748,7 @@ static void stats_layout(bgv_stats* s, const dev_batch& d) {
   s->lines = d.lines;
   s->defer_from = d.defer_grp ? d.defer_from : d.n_sets;
   s->clear_lanes = d.clear_lanes;
+  s->miller_kv = d.miller_kv;
 }
 
 // job results, set codes and the batch flag through pinned memory; the

@@ -28,6 +28,7 @@ struct dev_batch {
                             // digit)-lane MSM (k_msm_digit)
   uint32_t split;           // 1: latency mode: hash maps on two lanes per set, subgroup check beside [r_i] sigma_i
   uint32_t clear_lanes;     // latency mode: lanes per point of the cofactor clearing (9, or 3)
+  uint32_t miller_kv;       // latency mode: 0, or the slots S of the two-pair Miller loop in views (k_miller_kv, 3 S lanes)
   uint32_t prefold_log2;    // >0: two-level job fold, groups of 2^prefold_log2 sets (k_job_prefold); 0: one level
   uint32_t lines;           // one-lane Miller loop over fixed-argument lines: the hash stream stores every set's
                             // 68 unevaluated lines (launch_lines), k_miller evaluates them at P (pairing.h)
@@ -136,6 +137,8 @@ void launch_hash_clear_coop(hipStream_t st, const dev_batch& b, const dev_work& 
 void launch_hash_clear_trio(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_latency.hip
 void launch_s_level_coop(hipStream_t st, const dev_batch& b, const dev_work& w, uint32_t s);  // bgv_latency.hip
 void launch_msm_job_coop(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_latency.hip
+void launch_pk_coop(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_latency.hip
+void launch_miller_kv(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_miller.hip
 void launch_fp12_tail(hipStream_t st, int stage, const dev_batch& b, const dev_work& w);  // bgv_tail.hip
 void launch_combine_final(hipStream_t st, const fp12_t* parts, uint32_t n, uint32_t* flag);
 void launch_final_exp_many(hipStream_t st, const fp12_t* in, fp12_t* out, uint32_t n);  // bgv_debug_stages

@@ -318,6 +318,12 @@ __global__ void BGV_BULK k_job_recode(dev_batch b, dev_work w) {
 #ifndef BGV_MSM_JOB_COOP
 #define BGV_MSM_JOB_COOP 1
 #endif
+#ifndef BGV_PK_COOP
+#define BGV_PK_COOP 1
+#endif
+#ifndef PK_COOP_MAX
+#define PK_COOP_MAX 9000u  // 3,136 sets: 7.20 -> 6.68 ms; at 12,544 its waves slow the clearing (9.7 -> 10.3 ms)
+#endif
 #ifndef BGV_MSM_JOB_COOP_BULK
 #define BGV_MSM_JOB_COOP_BULK 0
 #endif
@@ -1126,7 +1132,7 @@ void launch_prep(hipStream_t st, const dev_batch& b, const dev_work& w) {
   BGV_LAUNCH(k_chunk_count, b.n_sets, b, w);
   if (b.n_sets) hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, w.chunk_off, b.n_sets);
   BGV_LAUNCH(k_chunk_set, b.n_sets, b, w);
-  if (!b.miller_coop) {
+  if (!b.miller_coop || b.miller_kv) {
     BGV_LAUNCH(k_item_count, b.n_jobs, b, w);
     if (b.n_jobs) hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, w.item_off, b.n_jobs);
     BGV_LAUNCH(k_item_job, b.n_jobs, b, w);
@@ -1198,7 +1204,9 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       launch_pk_gather(st, b, w);  // bgv_gather.hip
       break;
     case ST_PK_SCALE:
-      BGV_LAUNCH(k_pk, b.n_sets, b, w);
+      // latency mode: three lanes per set (bgv_latency.hip k_pk_coop)
+      if (b.split && BGV_PK_COOP && b.n_sets < PK_COOP_MAX) launch_pk_coop(st, b, w);
+      else BGV_LAUNCH(k_pk, b.n_sets, b, w);
       break;
     case ST_SIG_SCALE:
       if (b.split && !b.msm) break;  // [r_i] sigma_i already ran in k_sig_split
@@ -1239,6 +1247,10 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       BGV_LAUNCH(k_job_s, b.n_jobs, b, w, span);
       break;
     case ST_MILLER:  // (r_i PK_i, H(m_i)) pairs: needs ST_HASH and ST_PK only
+      if (b.miller_kv) {
+        launch_miller_kv(st, b, w);  // bgv_miller.hip
+        break;
+      }
       if (b.miller_coop == 2) {
         launch_miller_duo(st, b, w);  // bgv_miller.hip
         break;

@@ -25,12 +25,16 @@
 #include "bgv_internal.h"
 #include "coop_g2.h"
 #include "kv_g2.h"
+#include "coop_g1.h"
 
 #ifndef BGV_KV_CLEAR
 #define BGV_KV_CLEAR 1  // three-lane clearing in views (kv_g2.h)
 #endif
 #ifndef BGV_KV9
 #define BGV_KV9 1  // nine-lane G2 kernels in views (kv_g2.h)
+#endif
+#ifndef BGV_KV9_LEVEL
+#define BGV_KV9_LEVEL 0
 #endif
 
 namespace bgv {
@@ -182,6 +186,61 @@ __global__ void __launch_bounds__(64, 1) k_sig_split_kv9(dev_batch b, dev_work w
   }
 }
 
+// k_pk (bgv_kernels.hip) on three lanes per set (coop_g1.h): the chunk sums
+// folded per set, then [r_i] PK_i and the affine conversion.  The latency
+// mode's path to the Miller loop waits for it (3,136 sets: one-lane k_pk
+// 1.6 ms after the gather, while the hash chain ends ~0.6 ms earlier).
+constexpr int G1C_GROUPS = 21;
+__global__ void __launch_bounds__(64, 1) k_pk_coop(dev_batch b, dev_work w) {
+  __shared__ g1c_scratch sm[G1C_GROUPS + 1];
+  __shared__ g1j tabs[G1C_GROUPS][16];
+  const uint32_t lane = threadIdx.x, grp = lane / 3u, s = lane % 3u;
+  const uint32_t i0 = blockIdx.x * G1C_GROUPS + grp;
+  const bool own = grp < (uint32_t)G1C_GROUPS && i0 < b.n_sets;
+  const uint32_t i = own ? i0 : 0u;
+  const g1c_grp g{&sm[grp], s};
+  g1j acc;
+  jac_set_inf(acc);
+  const uint32_t c0 = w.chunk_off[i], c1 = w.chunk_off[i + 1];
+  bool range_err = c1 > b.chunk_bound || b.pk_off[i + 1] < b.pk_off[i];
+  const uint32_t cend = range_err ? c0 : c1;
+  // the wave walks its longest chunk list together (rounds stay wave-wide)
+  uint32_t nmax = cend - c0;
+  for (uint32_t off = 32; off >= 1; off >>= 1) nmax = max(nmax, (uint32_t)__shfl_xor((int)nmax, off, 64));
+  for (uint32_t k = 0; k < nmax; k++) {
+    const bool live = c0 + k < cend;
+    g1j pp;
+    if (live) pp = w.pk_part[c0 + k];
+    else jac_set_inf(pp);
+    if (live && !jac_is_inf(pp) && fp_is_zero(pp.x)) range_err = true;
+    g1c_add(g, acc, acc, pp);
+  }
+  int32_t code = C_OK;
+  if (range_err) code = C_INDEX_RANGE;
+  else if (jac_is_inf(acc)) code = C_PK_IS_INFINITY;
+  g1a out;
+  if (w.pk_agg && own && s == 0) {  // bgv_debug_stages: the aggregate before scaling
+    if (code != C_OK || !jac_to_aff(out, acc)) { fp_set_zero(out.x); fp_set_zero(out.y); }
+    w.pk_agg[i] = out;
+  }
+  g1j rp;
+  g1c_mul_u64_w4(g, tabs[grp < (uint32_t)G1C_GROUPS ? grp : G1C_GROUPS - 1u], grp < (uint32_t)G1C_GROUPS, rp, acc,
+                 b.scalars[i]);
+  if (!own || s != 0) return;
+  if (code == C_OK) {
+    jac_to_aff(out, rp);
+  } else {
+    fp_set_zero(out.x);
+    fp_set_zero(out.y);
+  }
+  w.rpk_aff[i] = out;
+  w.pk_code[i] = code;
+}
+
+void launch_pk_coop(hipStream_t st, const dev_batch& b, const dev_work& w) {
+  if (b.n_sets) hipLaunchKernelGGL(k_pk_coop, dim3((b.n_sets + G1C_GROUPS - 1) / G1C_GROUPS), dim3(64), 0, st, b, w);
+}
+
 void launch_hash_clear_trio(hipStream_t st, const dev_batch& b, const dev_work& w) {
   if (!b.n_sets) return;
   if (BGV_KV_CLEAR)
@@ -302,7 +361,10 @@ void launch_msm_job_coop(hipStream_t st, const dev_batch& b, const dev_work& w) 
 
 void launch_s_level_coop(hipStream_t st, const dev_batch& b, const dev_work& w, uint32_t s) {
   if (!b.n_sets) return;
-  if (BGV_KV9) hipLaunchKernelGGL(k_s_level_kv9, dim3((b.n_sets + KV3_GROUPS - 1) / KV3_GROUPS), dim3(64), 0, st, b, w, s);
+  // the one-addition levels stay on coop_g2.h: the view form's load and
+  // gather of a lone addition cost more than it saves (3,136 sets: 0.045
+  // against 0.027 ms per level)
+  if (BGV_KV9 && BGV_KV9_LEVEL) hipLaunchKernelGGL(k_s_level_kv9, dim3((b.n_sets + KV3_GROUPS - 1) / KV3_GROUPS), dim3(64), 0, st, b, w, s);
   else hipLaunchKernelGGL(k_s_level_coop, dim3((b.n_sets + CG_GROUPS - 1) / CG_GROUPS), dim3(64), 0, st, b, w, s);
 }
 

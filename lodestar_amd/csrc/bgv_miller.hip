@@ -44,6 +44,7 @@
 #include "bgv_internal.h"
 #include "miller_duo.h"
 #include "miller_quad.h"
+#include "miller_kv.h"
 
 namespace bgv {
 
@@ -149,6 +150,86 @@ __global__ void __launch_bounds__(64, 1) k_miller_quad(dev_batch b, dev_work w, 
 
 void launch_miller_quad(hipStream_t st, const dev_batch& b, const dev_work& w) {
   if (b.n_sets) hipLaunchKernelGGL(k_miller_quad, dim3((b.n_sets + 15u) / 16u), dim3(64), 0, st, b, w, b.n_sets);
+}
+
+// Two pairs per group of 3 S lanes in Karatsuba views (miller_kv.h): the
+// work items of k_miller (a job's sets two at a time, item_off / item_job),
+// f_set[i1] = f_{x,Q1}(P1) f_{x,Q2}(P2) and f_set[i1 + 1] = 1 (as k_miller)
+template <int S>
+__global__ void __launch_bounds__(64, 1) k_miller_kv(dev_batch b, dev_work w) {
+  constexpr int LANES = 3 * S, G = 64 / LANES;
+  __shared__ mkv_scratch sm[G + 1];
+  const uint32_t lane = threadIdx.x, grp = lane / LANES, r = lane % LANES, s = r / 3u, q = r % 3u;
+  const uint32_t n_items = w.item_off[b.n_jobs];
+  const uint32_t t0 = blockIdx.x * G + grp;
+  const bool own = grp < (uint32_t)G && t0 < n_items;
+  const uint32_t t = own ? t0 : 0u;
+  const mkv_grp<S> g{&sm[grp], s, q};
+  if (s == 0 && q == 0) {
+    fp_t z;
+    fp_set_zero(z);
+    lds_put(&((BGV_LDS mkv_scratch*)g.sc)->Z, z);
+  }
+  coop_wave_sync();
+  const uint32_t j = w.item_job[t];
+  const uint32_t i1 = b.job_off[j] + 2u * (t - w.item_off[j]);
+  const bool two = i1 + 1u < b.job_off[j + 1];
+  const uint32_t idx[2] = {i1, two ? i1 + 1u : i1};
+  mkv_pair T[2];
+  fp_t qx[2], qy[2];
+  const fp_t one = mkv_one(q);
+#pragma unroll
+  for (int p = 0; p < 2; p++) {
+    const g1a P = w.rpk_aff[idx[p]];
+    const g2a Q = w.h_aff[idx[p]];
+    qx[p] = kv_view(Q.x, q);
+    qy[p] = kv_view(Q.y, q);
+    T[p].x = qx[p];
+    T[p].y = qy[p];
+    T[p].z = one;
+    T[p].xp = P.x;
+    T[p].yp = P.y;
+  }
+  fp_t fa[3], fb[3];
+  mkv_miller2<S>(g, T, qx, qy, two, fa, fb);
+  if (!own || s != 0 || q > 1) return;
+  // a rejected pubkey rejects the job: its Miller values are never used (1, as k_miller)
+  const bool ok = w.pk_code[i1] == C_OK && (!two || w.pk_code[i1 + 1u] == C_OK);
+  // views 0 and 1 are the components: each of the two lanes writes its own
+  fp12_t* f = &w.f_set[i1];
+  fp2_t* cs[6] = {&f->c0.c0, &f->c0.c1, &f->c0.c2, &f->c1.c0, &f->c1.c1, &f->c1.c2};
+  const fp_t* vs[6] = {&fa[0], &fa[1], &fa[2], &fb[0], &fb[1], &fb[2]};
+  fp_t z;
+  fp_set_zero(z);
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const fp_t v = ok ? *vs[k] : ((k == 0 && q == 0) ? FP_ONE : z);
+    if (q) cs[k]->c1 = v;
+    else cs[k]->c0 = v;
+  }
+  if (two) {
+    fp12_t* f2 = &w.f_set[i1 + 1u];
+    fp2_t* ds[6] = {&f2->c0.c0, &f2->c0.c1, &f2->c0.c2, &f2->c1.c0, &f2->c1.c1, &f2->c1.c2};
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      const fp_t v = (k == 0 && q == 0) ? FP_ONE : z;
+      if (q) ds[k]->c1 = v;
+      else ds[k]->c0 = v;
+    }
+  }
+}
+
+void launch_miller_kv(hipStream_t st, const dev_batch& b, const dev_work& w) {
+  // items <= n_sets / 2 + n_jobs (a job of odd size leaves a one-pair item)
+  const uint32_t items = b.n_sets / 2u + b.n_jobs;
+  if (!items) return;
+  if (b.miller_kv == 6) {
+    constexpr uint32_t G = 64 / 18;
+    hipLaunchKernelGGL(k_miller_kv<6>, dim3((items + G - 1) / G), dim3(64), 0, st, b, w);
+  } else {
+    constexpr uint32_t G = 64 / 9;
+    hipLaunchKernelGGL(k_miller_kv<3>, dim3((items + G - 1) / G), dim3(64), 0, st, b, w);
+  }
 }
 
 // the unevaluated lines of every set's H(m) (pairing.h miller_lines), on the

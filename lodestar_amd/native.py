@@ -94,8 +94,9 @@ class BgvStats(ctypes.Structure):
         ("lines", ctypes.c_uint32),
         ("defer_from", ctypes.c_uint32),
         ("clear_lanes", ctypes.c_uint32),
+        ("miller_kv", ctypes.c_uint32),
     ]
-    LAYOUT = ("split", "miller_lanes", "pairs_per_item", "msm", "lines", "defer_from", "clear_lanes")
+    LAYOUT = ("split", "miller_lanes", "pairs_per_item", "msm", "lines", "defer_from", "clear_lanes", "miller_kv")
 
     def as_dict(self, lib=None):
         names = [lib.stage_name(i) for i in range(N_STAGES)] if lib else [str(i) for i in range(N_STAGES)]
@@ -120,9 +121,10 @@ class BgvCfg(ctypes.Structure):
     Production contexts use the defaults (every field "auto")."""
     _fields_ = [("struct_size", ctypes.c_uint32)] + [
         (k, ctypes.c_int32) for k in
-        ("split", "miller", "job_lanes", "msm", "pairs", "prefold", "lines", "defer_pct", "timing", "clear_lanes")]
+        ("split", "miller", "job_lanes", "msm", "pairs", "prefold", "lines", "defer_pct", "timing", "clear_lanes",
+         "miller_kv")]
     AUTO = {"split": -1, "miller": -1, "job_lanes": 0, "msm": -1, "pairs": 0, "prefold": -1, "lines": -1,
-            "defer_pct": -1, "timing": -1, "clear_lanes": -1}
+            "defer_pct": -1, "timing": -1, "clear_lanes": -1, "miller_kv": -1}
 
     @classmethod
     def make(cls, **over) -> "BgvCfg":

@@ -37,6 +37,9 @@ MODES = {
     "bulk_serial_msm": {"split": 0, "miller": 1, "msm": 1, "pairs": 1},
     "c4_path": {"split": 0, "miller": 1, "msm": 2, "pairs": 2},
     "bulk_msm4": {"split": 0, "miller": 1, "msm": 4, "pairs": 1},
+    # two-pair Miller loop in Karatsuba views (miller_kv.h), 9 and 18 lanes per two pairs
+    "kv3_clear3_msm4": {"split": 1, "miller_kv": 3, "msm": 4, "clear_lanes": 3},
+    "kv6_clear9": {"split": 1, "miller_kv": 6, "clear_lanes": 9},
 }
 
 
@@ -82,7 +85,7 @@ def test_stage_values_match_oracle(golden, mode):
     # set pairs: one Miller value per set, or (two pairs per work item) the
     # item's product at its first set and the identity at its second; an item
     # with a rejected pubkey contributes the identity
-    pairs = MODES[mode].get("pairs", 1) == 2
+    pairs = MODES[mode].get("pairs", 1) == 2 or MODES[mode].get("miller_kv", 0) > 0
     jo = arrays["job_offsets"]
     for j in range(J):
         beg, end = int(jo[j]), int(jo[j + 1])

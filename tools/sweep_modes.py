@@ -78,6 +78,9 @@ MODES = {  # bgv_cfg overrides (include/bgv.h)
     "nolines": {"lines": 0},
     "p2": {"pairs": 2},
     "p2l": {"pairs": 2, "lines": 1},
+    "kv3": {"miller_kv": 3},
+    "kv6": {"miller_kv": 6},
+    "kv0": {"miller_kv": 0},
 }
 
 
