@@ -204,6 +204,93 @@ __device__ void c_mul(wfp12* out, const wfp12* a, const wfp12* b, cscratch* s) {
 }
 #endif
 
+// acc = acc^2 for acc in the cyclotomic subgroup (after the easy part of the
+// final exponentiation): Granger-Scott over Fp4 = Fp2[s]/(s^2 - xi), s = w^3,
+// with fp12_cyclotomic_sqr's formulas (fp12.h) and pairs (w^p, w^(p+3)),
+// p = 0, 1, 2.  Its nine Fp2 squarings are one Fp squaring per lane in
+// Karatsuba views (kv_g2.h), so a squaring is one product deep instead of
+// c_mul's 108-product round and cross-lane sum.  Wave 0 only:
+//   R1 lane 3m + q (m < 9): pair p = m / 3, x = a | b | a + b (m % 3),
+//      P[m][q] = v_q(x)^2 with v0 = x0, v1 = x1, v2 = x0 + x1
+//   R2 lane 2m + c (m < 9): component c of x_m^2: P0 - P1 | P2 - (P0 + P1)
+//   R3 lane 2k + c (k < 6): component c of w^k' = 3 t_k -+ 2 w^k with
+//      t = a^2 + xi b^2 of pair k / 2 (k even, minus), (a + b)^2 - a^2 - b^2
+//      of pair 0 (k = 3) or 1 (k = 5), xi times it of pair 2 (k = 1) (plus)
+// Canonical residues in and out: bit-identical to c_mul(acc, acc, acc) (GPU
+// stage tests green with it on).  Off: a lone wave's latency is its
+// instruction count, and the squaring's linear combinations (R3: up to seven
+// modular multi-ops and the operand selects on one lane) cost about what
+// c_mul's 108-lane round and cross-lane sum do: k_batch_final 1.20-1.39 ms
+// with it against 1.23-1.27 without (r04, profiles/r04c_ab_fe_cyc.txt).
+#ifndef BGV_FE_CYC
+#define BGV_FE_CYC 0
+#endif
+__device__ __forceinline__ void c_wave_fence() { __builtin_amdgcn_wave_barrier(); __asm__ volatile("" ::: "memory"); }
+__device__ void c_cyc_sqr(wfp12* acc_, cscratch* s_) {
+  BGV_LDS wfp12* acc = (BGV_LDS wfp12*)acc_;
+  BGV_LDS cscratch* s = (BGV_LDS cscratch*)s_;
+  const uint32_t l = threadIdx.x;
+  if (l < 64) {
+    if (l < 27) {
+      const uint32_t m = l / 3, q = l - 3 * m, p = m / 3, kind = m - 3 * p;
+      const fp_t a0 = lds_get(&acc->c[p].c0), a1 = lds_get(&acc->c[p].c1);
+      const fp_t b0 = lds_get(&acc->c[p + 3].c0), b1 = lds_get(&acc->c[p + 3].c1);
+      fp_t s0, s1;
+      fp_add2(s0, a0, b0, s1, a1, b1);
+      const fp_t& x0 = kind == 0 ? a0 : (kind == 1 ? b0 : s0);
+      const fp_t& x1 = kind == 0 ? a1 : (kind == 1 ? b1 : s1);
+      fp_t v2;
+      fp_add_lazy(v2, x0, x1);  // < 2p, product input only
+      const fp_t& v = q == 0 ? x0 : (q == 1 ? x1 : v2);
+      fp_t r;
+      fp_sqr(r, v);
+      lds_put(&s->p[l], r);
+    }
+    c_wave_fence();
+    if (l < 18) {
+      const uint32_t m = l >> 1, c = l & 1u;
+      const fp_t p0 = lds_get(&s->p[3 * m]), p1 = lds_get(&s->p[3 * m + 1]), p2 = lds_get(&s->p[3 * m + 2]);
+      fp_t w;
+      fp_add(w, p0, p1);
+      fp_t r;
+      fp_sub(r, c ? p2 : p0, c ? w : p1);
+      lds_put(c ? &s->q[m].c1 : &s->q[m].c0, r);
+    }
+    c_wave_fence();
+    if (l < 12) {
+      const uint32_t k = l >> 1, c = l & 1u;
+      const bool odd = k & 1u;
+      // squares of the pair: A = a^2, B = b^2, C = (a + b)^2 (both components)
+      const uint32_t pr = odd ? (k == 3 ? 0u : (k == 5 ? 1u : 2u)) : k >> 1;
+      const fp2_t A = {lds_get(&s->q[3 * pr].c0), lds_get(&s->q[3 * pr].c1)};
+      const fp2_t B = {lds_get(&s->q[3 * pr + 1].c0), lds_get(&s->q[3 * pr + 1].c1)};
+      const fp2_t C = {lds_get(&s->q[3 * pr + 2].c0), lds_get(&s->q[3 * pr + 2].c1)};
+      fp_t t;
+      if (!odd) {  // (a^2 + xi b^2)_c = A_c + (B0 -+ B1)
+        fp_t bs, bd;
+        fp_add_sub(bs, B.c0, B.c1, bd, B.c0, B.c1);
+        fp_add(t, c ? A.c1 : A.c0, c ? bs : bd);
+      } else {  // r = C - A - B; t = r_c, or (xi r)_c = r0 -+ r1 for k = 1
+        fp_t u0, u1, r0, r1;
+        fp_add2(u0, A.c0, B.c0, u1, A.c1, B.c1);
+        fp_sub2(r0, C.c0, u0, r1, C.c1, u1);
+        fp_t xs, xd;
+        fp_add_sub(xs, r0, r1, xd, r0, r1);
+        t = k == 1 ? (c ? xs : xd) : (c ? r1 : r0);
+      }
+      // 3 t - 2 z (k even) or 3 t + 2 z (k odd) = 2 (t -+ z) + t
+      const fp_t z = lds_get(c ? &acc->c[k].c1 : &acc->c[k].c0);
+      fp_t ts, td;
+      fp_add_sub(ts, t, z, td, t, z);
+      fp_t u = odd ? ts : td, o;
+      fp_add(u, u, u);
+      fp_add(o, u, t);
+      lds_put(c ? &acc->c[k].c1 : &acc->c[k].c0, o);
+    }
+  }
+  __syncthreads();
+}
+
 __device__ void c_set_one(wfp12* r) {
   const uint32_t l = threadIdx.x;
   if (l < 6) r->c[l] = l == 0 ? fp2_one() : fp2_zero();
@@ -282,7 +369,11 @@ __device__ void c_frob(wfp12* out, const wfp12* a, int k, cscratch* s) {
 __device__ void c_pow_x(wfp12* out, const wfp12* a, wfp12* acc, cscratch* s) {
   c_copy(acc, a);
   for (int b = 62; b >= 0; b--) {
+#if BGV_FE_CYC
+    c_cyc_sqr(acc, s);
+#else
     c_mul(acc, acc, acc, s);
+#endif
     if ((BLS_X_ABS >> b) & 1ull) c_mul(acc, acc, a, s);
   }
   c_conj(out, acc);

@@ -22,7 +22,7 @@ sys.path.insert(0, ROOT)
 CALLS = os.path.join(ROOT, "gpurun_out", "size_trace_calls.json")
 
 
-def run(sizes, reps, cfg):
+def run(sizes, reps, cfg, single=0):
     import numpy as np
     import torch
 
@@ -51,6 +51,16 @@ def run(sizes, reps, cfg):
             calls.append(n)
         print(json.dumps({"sets": n, "ms_p50": round(float(np.median(t[1:])) * 1e3, 3)}), flush=True)
         time.sleep(0.05)
+    if single:  # one host-resident set per call (bench.py single_set_latency_ms)
+        arr = bench.signed(d, bench.singles(1, bench.SEED + 3500))
+        t = []
+        for r in range(1 + single):
+            t1 = time.perf_counter()
+            jr, _ = d.verify(arr, on_device=False, want_set_codes=False)
+            t.append(time.perf_counter() - t1)
+            assert (jr == 1).all()
+            calls.append(1)
+        print(json.dumps({"sets": 1, "host": True, "ms_p50": round(float(np.median(t[1:])) * 1e3, 3)}), flush=True)
     d.close()
     os.makedirs(os.path.dirname(CALLS), exist_ok=True)
     json.dump(calls, open(CALLS, "w"))
@@ -82,13 +92,14 @@ def main():
     ap.add_argument("--sizes", default="3136,12544")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cfg", default="{}", help="bgv_cfg overrides as JSON, e.g. '{\"miller\": 2}'")
+    ap.add_argument("--single", type=int, default=0, help="also time this many host-resident one-set calls")
     ap.add_argument("--analyze")
     ap.add_argument("--calls", default=CALLS)
     a = ap.parse_args()
     if a.analyze:
         analyze(a.analyze, a.calls)
     else:
-        run([int(x) for x in a.sizes.split(",")], a.reps, json.loads(a.cfg))
+        run([int(x) for x in a.sizes.split(",") if x], a.reps, json.loads(a.cfg), a.single)
 
 
 if __name__ == "__main__":
