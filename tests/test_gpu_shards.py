@@ -5,7 +5,9 @@ pipeline layouts (no bgv_cfg overrides), through both device paths:
     (four-lane Miller loop, three-lane cofactor clearing, digit MSM, deferred
     subgroup checks at the time of writing), and
   * the one-epoch slice, 32 blocks = 3,136 sets (the batch range sync issues,
-    sync/constants.ts:41; cooperative Miller loop, nine-lane clearing),
+    sync/constants.ts:41; two-pair view Miller loop on 18 lanes, nine-lane
+    view clearing), and the two other view-Miller ranges: 16 blocks = 1,568
+    sets (18 lanes per two pairs) and 64 blocks = 6,272 sets (9 lanes),
 
 each with 1 % faults of the four C5 kinds (bench.inject_faults: wrong message,
 swapped pubkey, cleared compression flag, on-curve point outside G2):
@@ -45,7 +47,7 @@ def dev():
 
 
 # blocks -> the layout prepare() picks by default at that size (bgv_api.hip)
-SIZES = {128: "c4_over_8", 32: "epoch_slice"}
+SIZES = {128: "c4_over_8", 64: "view_miller_9_lanes", 32: "epoch_slice", 16: "view_miller_18_lanes"}
 
 
 @pytest.mark.parametrize("blocks", sorted(SIZES))
