@@ -186,7 +186,7 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
     if (k.msm < -1 || k.msm > 4) return fail(BGV_E_INVALID_ARG, "bgv_cfg.msm %d", k.msm);
     if (k.clear_lanes != -1 && k.clear_lanes != 1 && k.clear_lanes != 3 && k.clear_lanes != 9)
       return fail(BGV_E_INVALID_ARG, "bgv_cfg.clear_lanes %d", k.clear_lanes);
-    if (k.miller_kv != -1 && k.miller_kv != 0 && k.miller_kv != 3 && k.miller_kv != 6)
+    if (k.miller_kv != -1 && k.miller_kv != 0 && k.miller_kv != 3 && k.miller_kv != 6 && k.miller_kv != 9)
       return fail(BGV_E_INVALID_ARG, "bgv_cfg.miller_kv %d", k.miller_kv);
     if (k.defer_pct < -1 || k.defer_pct > 100) return fail(BGV_E_INVALID_ARG, "bgv_cfg.defer_pct %d", k.defer_pct);
     auto tri_ok = [](int v) { return v >= -1 && v <= 1; };

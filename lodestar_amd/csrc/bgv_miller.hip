@@ -223,7 +223,10 @@ void launch_miller_kv(hipStream_t st, const dev_batch& b, const dev_work& w) {
   // items <= n_sets / 2 + n_jobs (a job of odd size leaves a one-pair item)
   const uint32_t items = b.n_sets / 2u + b.n_jobs;
   if (!items) return;
-  if (b.miller_kv == 6) {
+  if (b.miller_kv == 9) {
+    constexpr uint32_t G = 64 / 27;
+    hipLaunchKernelGGL(k_miller_kv<9>, dim3((items + G - 1) / G), dim3(64), 0, st, b, w);
+  } else if (b.miller_kv == 6) {
     constexpr uint32_t G = 64 / 18;
     hipLaunchKernelGGL(k_miller_kv<6>, dim3((items + G - 1) / G), dim3(64), 0, st, b, w);
   } else {

@@ -236,6 +236,28 @@ def _ptr(a) -> int | None:
     return int(a.data_ptr())  # torch tensor (device-resident)
 
 
+def _sync_producers(*objs) -> None:
+    """Device-resident inputs must be complete before the library reads them
+    (include/bgv.h, bgv_batch.on_device): the library runs on its own streams,
+    which do not wait for the stream that produced a torch tensor.  Wait for
+    the current torch stream of every device a tensor argument lives on (a
+    tensor filled by torch.full / torch.zeros / a copy is otherwise still being
+    written when the library's kernels read it, or -- for an output buffer --
+    overwrites what they wrote)."""
+    seen = set()
+    for o in objs:
+        vals = o.values() if isinstance(o, dict) else (o,)
+        for a in vals:
+            if a is None or isinstance(a, (np.ndarray, bytes, bytearray, int, float, str)):
+                continue
+            dev = getattr(a, "device", None)
+            if dev is None or getattr(dev, "type", "") != "cuda" or dev in seen:
+                continue
+            seen.add(dev)
+            import torch
+            torch.cuda.current_stream(dev).synchronize()
+
+
 class Device:
     """One bgv_ctx: a HIP device, its stream and its HBM pubkey table."""
 
@@ -315,6 +337,8 @@ class Device:
         b.sig_len = _ptr(arrays.get("sig_len"))
         b.scalars = _ptr(arrays.get("scalars"))
         b.on_device = 1 if on_device else 0
+        if on_device:
+            _sync_producers(arrays)
         return b
 
     def verify(self, arrays: dict, on_device: bool = False, want_set_codes: bool = True):
@@ -372,6 +396,7 @@ class Device:
         return bool(r.value)
 
     def gen_sign(self, arrays: dict, out, on_device: bool = False):
+        _sync_producers(out)
         b = self.make_batch(arrays, on_device)
         self._check(self.lib.bgv_gen_sign(self.h, ctypes.byref(b), _ptr(out)))
 

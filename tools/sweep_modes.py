@@ -80,6 +80,7 @@ MODES = {  # bgv_cfg overrides (include/bgv.h)
     "p2l": {"pairs": 2, "lines": 1},
     "kv3": {"miller_kv": 3},
     "kv6": {"miller_kv": 6},
+    "kv9": {"miller_kv": 9},
     "kv0": {"miller_kv": 0},
 }
 
