@@ -502,7 +502,7 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   //    (37,632: 25.1 -> 22.5 ms; 50,176: 26.0 -> 24.9 ms)
   static const uint32_t MILLER18_MIN = 2000, MILLER4_MIN = 6000, MILLER2_MIN = 18000, MILLER1_MIN = 35000,
                         MSM_MIN = 6000, MSM4_MIN = 9000, MSM2_MIN = 35000, SPLIT_MAX = 65536, PAIRS2_MIN = 65536,
-                        CLEAR3_MIN = 9000, KV6_MIN = 1200, KV3_MIN = 4500, KV_MAX = 11500;
+                        CLEAR3_MIN = 9000, KV6_MIN = 1100, KV3_MIN = 4500, KV_MAX = 11500;
   const bgv_cfg& k = c->cfg;
   d.pairs_per_item = k.pairs ? (uint32_t)k.pairs : (n >= PAIRS2_MIN ? 2u : 1u);
   d.split = k.split >= 0 ? (uint32_t)k.split : (n < SPLIT_MAX ? 1u : 0u);
@@ -556,10 +556,12 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   {
     // r04 sweeps (profiles/r04_sweep_kv.txt, r04c_sweep_kv_bounds.txt): 1,960
     // sets 7.57 -> 6.42 ms and 3,136 sets 6.68 -> 6.57 ms with 18 lanes per two
-    // pairs (980 sets: 6.08 -> 6.31, so not below ~1,200); 4,704 sets 7.98 ->
+    // pairs (980 sets: 6.02 -> 6.18, 1,176 sets 6.70 -> 6.20: from 1,100); 4,704 sets 7.98 ->
     // 7.87, 6,272 sets 8.88 -> 8.48 ms and 10,976 sets 9.38 -> 9.17 ms with 9;
     // at 12,544 the four-lane one-pair loop stays (9.7 against 10.8 ms: the
-    // 9-lane groups' 915 waves leave no SIMD to the checks and the signature chain)
+    // 9-lane groups' 915 waves leave no SIMD to the checks and the signature chain).
+    // 27 lanes per two pairs (miller_kv = 9) ties 18 at 980-1,960 sets and loses
+    // from 3,136 (7.05 against 6.52 ms; profiles/r04e_sweep_kv9.txt): A/B only
     const uint32_t auto_kv = n >= KV6_MIN && n < KV3_MIN ? 6u : (n >= KV3_MIN && n < KV_MAX ? 3u : 0u);
     d.miller_kv = k.miller_kv >= 0 ? (uint32_t)k.miller_kv : auto_kv;
     if (!d.split) d.miller_kv = 0;
