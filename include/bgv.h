@@ -171,7 +171,7 @@ typedef struct bgv_cfg {
   int32_t defer_pct;    /* -1 auto; 0..100: share of the G2 subgroup checks run beside the Miller loops (bulk mode) */
   int32_t timing;       /* -1 auto (batches >= 65,536 sets); 0 / 1 per-stage timing events */
   int32_t clear_lanes;  /* -1 auto; 1 / 3 / 9 lanes per point of the latency mode's cofactor clearing */
-  int32_t miller_kv;    /* -1 auto; 0 off; 3 / 6 / 9: the two-pair Miller loop in Karatsuba views on 9 / 18 / 27 lanes per two pairs */
+  int32_t miller_kv;    /* -1 auto; 0 off; 2 / 3 / 6 / 9: the two-pair Miller loop in Karatsuba views on 6 / 9 / 18 / 27 lanes per two pairs */
 } bgv_cfg;
 /* every field "auto" */
 void bgv_cfg_default(bgv_cfg* cfg);

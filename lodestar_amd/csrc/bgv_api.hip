@@ -73,6 +73,7 @@ struct bgv_ctx {
   hipEvent_t ev_prep = nullptr;       // end of launch_prep (latency batches fork the hash leg before it)
   hipEvent_t ev_sigdec = nullptr;     // defer_grp: signatures decoded (the checks may start)
   hipEvent_t ev_grp = nullptr;        // defer_grp: subgroup checks done (the code fix-up may start)
+  hipEvent_t ev_maps = nullptr;       // early_maps: the hash maps on st_hash are done
   hipEvent_t ev_dep[ST_COUNT] = {};   // untimed cross-stream dependencies (latency batches)
   // index2pubkey table (grown by copy) and synthetic secret keys
   g1a* table = nullptr;
@@ -186,7 +187,7 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
     if (k.msm < -1 || k.msm > 4) return fail(BGV_E_INVALID_ARG, "bgv_cfg.msm %d", k.msm);
     if (k.clear_lanes != -1 && k.clear_lanes != 1 && k.clear_lanes != 3 && k.clear_lanes != 9)
       return fail(BGV_E_INVALID_ARG, "bgv_cfg.clear_lanes %d", k.clear_lanes);
-    if (k.miller_kv != -1 && k.miller_kv != 0 && k.miller_kv != 3 && k.miller_kv != 6 && k.miller_kv != 9)
+    if (k.miller_kv != -1 && k.miller_kv != 0 && k.miller_kv != 2 && k.miller_kv != 3 && k.miller_kv != 6 && k.miller_kv != 9)
       return fail(BGV_E_INVALID_ARG, "bgv_cfg.miller_kv %d", k.miller_kv);
     if (k.defer_pct < -1 || k.defer_pct > 100) return fail(BGV_E_INVALID_ARG, "bgv_cfg.defer_pct %d", k.defer_pct);
     auto tri_ok = [](int v) { return v >= -1 && v <= 1; };
@@ -221,6 +222,7 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
   HIPCHK(hipEventCreateWithFlags(&c->ev_prep, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&c->ev_sigdec, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&c->ev_grp, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&c->ev_maps, hipEventDisableTiming));
   *out = c;
   return BGV_OK;
 }
@@ -239,6 +241,7 @@ int bgv_close(bgv_ctx* c) {
   (void)hipEventDestroy(c->ev_prep);
   (void)hipEventDestroy(c->ev_sigdec);
   (void)hipEventDestroy(c->ev_grp);
+  (void)hipEventDestroy(c->ev_maps);
   if (c->pin_in) (void)hipHostFree(c->pin_in);
   if (c->pin_out) (void)hipHostFree(c->pin_out);
   if (c->table) (void)hipFree(c->table);
@@ -403,6 +406,37 @@ static int stage_issue(bgv_ctx* c, size_t total) {
   return 0;
 }
 
+// latency mode by batch size (prepare(); the r02 sweep: 25,088 sets 24.5 ms
+// split against 26.3 ms, 50,176: 35.4 against 29.3; r03: to 65,536)
+static const uint32_t SPLIT_MAX = 65536;
+static bool layout_split(const bgv_cfg& k, uint32_t n) { return k.split >= 0 ? k.split != 0 : n < SPLIT_MAX; }
+
+// The hash maps of a latency-mode batch read only the messages, and they head
+// the critical path (maps -> clearing -> Miller -> fold -> final exp): they are
+// launched on the hash stream as soon as the messages are on the device,
+// before the host reads back offsets, checks them and sets up the rest
+// (on-device batches: ~0.1 ms of idle GPU at 3,136 sets, r04c timeline).
+// Timed runs keep the maps inside the hash stage's events.
+#ifndef BGV_EARLY_MAPS
+#define BGV_EARLY_MAPS 1
+#endif
+static int early_maps(bgv_ctx* c, dev_batch& d, bool after_staging) {
+  const uint32_t n = d.n_sets;
+  if (!BGV_EARLY_MAPS) return 0;
+  const bool timed = c->cfg.timing >= 0 ? c->cfg.timing != 0 : n >= 65536;
+  if (!n || timed || !layout_split(c->cfg, n)) return 0;
+  if (int r = c->q_part.ensure(2 * (size_t)n)) return r;
+  if (after_staging) HIPCHK(hipStreamWaitEvent(c->st_hash, c->ev_staged, 0));
+  dev_work w;
+  memset(&w, 0, sizeof w);
+  w.q_part = c->q_part.p;
+  launch_hash_maps(c->st_hash, d, w);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev_maps, c->st_hash));
+  d.maps_early = 1;
+  return 0;
+}
+
 // Build the device view of a batch: stage host arrays, convert raw pubkeys.
 // Host batches: the arrays are copied into pinned memory FIRST and every
 // contract check reads that copy, so the device only ever sees checked
@@ -457,6 +491,8 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
     memcpy(c->jo_host.data(), jo, c->jo_host.size() * 4);
     c->pk_total = total;
     if (int r = stage_issue(c, bytes)) return r;
+    if (need_sigs)  // verification calls (bgv_gen_sign hashes on its own)
+      if (int r = early_maps(c, d, true)) return r;
     if (!b->scalars) d.scalars = nullptr;
     if (!need_sigs) { d.sigs = nullptr; d.sig_len = nullptr; }
     if (int r = c->raw_conv.ensure(b->n_raw ? b->n_raw : 1)) return r;
@@ -469,6 +505,8 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
     d.msgs = b->msgs;
     d.sigs = b->sigs;
     d.sig_len = b->sig_len;
+    if (need_sigs)
+      if (int r = early_maps(c, d, false)) return r;
     if (int r = c->raw_conv.ensure(b->n_raw ? b->n_raw : 1)) return r;
     launch_raw_pks(c->st, b->raw_pks, c->raw_conv.p, b->n_raw);
     d.raw_pks = c->raw_conv.p;
@@ -501,11 +539,11 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   //    one-lane Miller loop and the (job, window) MSM up to 65,536 sets
   //    (37,632: 25.1 -> 22.5 ms; 50,176: 26.0 -> 24.9 ms)
   static const uint32_t MILLER18_MIN = 2000, MILLER4_MIN = 6000, MILLER2_MIN = 18000, MILLER1_MIN = 35000,
-                        MSM_MIN = 6000, MSM4_MIN = 9000, MSM2_MIN = 35000, SPLIT_MAX = 65536, PAIRS2_MIN = 65536,
+                        MSM_MIN = 6000, MSM4_MIN = 9000, MSM2_MIN = 35000, PAIRS2_MIN = 65536,
                         CLEAR3_MIN = 9000, KV6_MIN = 1100, KV3_MIN = 4500, KV_MAX = 11500;
   const bgv_cfg& k = c->cfg;
   d.pairs_per_item = k.pairs ? (uint32_t)k.pairs : (n >= PAIRS2_MIN ? 2u : 1u);
-  d.split = k.split >= 0 ? (uint32_t)k.split : (n < SPLIT_MAX ? 1u : 0u);
+  d.split = layout_split(k, n) ? 1u : 0u;
   // one lane per point from 18,000 sets (25,088: 16.74 -> 16.5 ms; the trio's
   // 1,176 waves oversubscribe the SIMDs there)
   d.clear_lanes = k.clear_lanes > 0 ? (uint32_t)k.clear_lanes : (n < CLEAR3_MIN ? 9u : n < MILLER2_MIN ? 3u : 1u);
@@ -706,6 +744,9 @@ static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int fro
       if (s == ST_S_TREE || s == ST_MILLER) HIPCHK(hipStreamWaitEvent(st, dep[ST_PK_SCALE], 0));
       if (s == ST_F_TREE) HIPCHK(hipStreamWaitEvent(st, dep[ST_MILLER], 0));
     }
+    // maps launched early on st_hash: a hash stage on another stream (a run
+    // that does not fork, e.g. bgv_debug_stages' first range) waits for them
+    if (s == ST_HASH && d.maps_early && st != c->st_hash) HIPCHK(hipStreamWaitEvent(st, c->ev_maps, 0));
     if (timed) HIPCHK(hipEventRecord(c->ev[s], st));
     // deferred subgroup checks: their verdicts enter the codes before the fold
     if (s == ST_F_TREE && d.defer_grp) {

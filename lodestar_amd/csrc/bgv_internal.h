@@ -29,6 +29,7 @@ struct dev_batch {
   uint32_t split;           // 1: latency mode: hash maps on two lanes per set, subgroup check beside [r_i] sigma_i
   uint32_t clear_lanes;     // latency mode: lanes per point of the cofactor clearing (9, or 3)
   uint32_t miller_kv;       // latency mode: 0, or the slots S of the two-pair Miller loop in views (k_miller_kv, 3 S lanes)
+  uint32_t maps_early;      // latency mode: k_hash_map already launched by prepare() (bgv_api.hip early_maps)
   uint32_t prefold_log2;    // >0: two-level job fold, groups of 2^prefold_log2 sets (k_job_prefold); 0: one level
   uint32_t lines;           // one-lane Miller loop over fixed-argument lines: the hash stream stores every set's
                             // 68 unevaluated lines (launch_lines), k_miller evaluates them at P (pairing.h)
@@ -124,6 +125,7 @@ void launch_table_from_compressed(hipStream_t st, const uint8_t* in, g1a* out, u
 void launch_table_from_uncompressed(hipStream_t st, const uint8_t* in, g1a* out, uint32_t n, int32_t* codes);
 void launch_table_export(hipStream_t st, const g1a* tab, uint8_t* out, uint32_t n);
 void launch_pk_validate(hipStream_t st, const uint8_t* in, uint32_t n, int32_t* codes);
+void launch_hash_maps(hipStream_t st, const dev_batch& b, const dev_work& w);  // prepare(): before the set-up
 void launch_prep(hipStream_t st, const dev_batch& b, const dev_work& w);  // before ST_PK / ST_MILLER
 void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work& w);
 void launch_miller(hipStream_t st, const dev_batch& b, const dev_work& w);  // bgv_miller.hip

@@ -1128,6 +1128,12 @@ void launch_table_export(hipStream_t st, const g1a* tab, uint8_t* out, uint32_t 
 // items): launched before the stages fork onto their streams, while the GPU
 // is idle.  Under the bulk kernels the one-workgroup scan is starved of its
 // CU (rocprofv3: 20 ms instead of tens of microseconds).
+// the latency mode's hash maps, launched by prepare() before the host-side
+// set-up of the batch (bgv_api.hip early_maps): they read only the messages
+void launch_hash_maps(hipStream_t st, const dev_batch& b, const dev_work& w) {
+  BGV_LAUNCH(k_hash_map, 2u * b.n_sets, b, w);
+}
+
 void launch_prep(hipStream_t st, const dev_batch& b, const dev_work& w) {
   BGV_LAUNCH(k_chunk_count, b.n_sets, b, w);
   if (b.n_sets) hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, w.chunk_off, b.n_sets);
@@ -1188,7 +1194,7 @@ void launch_stage(hipStream_t st, int stage, const dev_batch& b, const dev_work&
       break;
     case ST_HASH:
       if (b.split) {
-        BGV_LAUNCH(k_hash_map, 2u * b.n_sets, b, w);
+        if (!b.maps_early) BGV_LAUNCH(k_hash_map, 2u * b.n_sets, b, w);
         if (b.clear_lanes == 3) {
           launch_hash_clear_trio(st, b, w);  // bgv_latency.hip
         } else if (BGV_COOP_G2 && b.clear_lanes != 1) {

@@ -229,6 +229,9 @@ void launch_miller_kv(hipStream_t st, const dev_batch& b, const dev_work& w) {
   } else if (b.miller_kv == 6) {
     constexpr uint32_t G = 64 / 18;
     hipLaunchKernelGGL(k_miller_kv<6>, dim3((items + G - 1) / G), dim3(64), 0, st, b, w);
+  } else if (b.miller_kv == 2) {
+    constexpr uint32_t G = 64 / 6;
+    hipLaunchKernelGGL(k_miller_kv<2>, dim3((items + G - 1) / G), dim3(64), 0, st, b, w);
   } else {
     constexpr uint32_t G = 64 / 9;
     hipLaunchKernelGGL(k_miller_kv<3>, dim3((items + G - 1) / G), dim3(64), 0, st, b, w);

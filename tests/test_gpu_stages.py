@@ -41,6 +41,7 @@ MODES = {
     "kv3_clear3_msm4": {"split": 1, "miller_kv": 3, "msm": 4, "clear_lanes": 3},
     "kv6_clear9": {"split": 1, "miller_kv": 6, "clear_lanes": 9},
     "kv9_clear9": {"split": 1, "miller_kv": 9, "clear_lanes": 9},
+    "kv2_clear3_msm4": {"split": 1, "miller_kv": 2, "msm": 4, "clear_lanes": 3},
 }
 
 

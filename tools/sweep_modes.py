@@ -81,6 +81,7 @@ MODES = {  # bgv_cfg overrides (include/bgv.h)
     "kv3": {"miller_kv": 3},
     "kv6": {"miller_kv": 6},
     "kv9": {"miller_kv": 9},
+    "kv2": {"miller_kv": 2},
     "kv0": {"miller_kv": 0},
 }
 
