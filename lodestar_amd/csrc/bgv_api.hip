@@ -67,6 +67,7 @@ struct bgv_ctx {
   int run_from = 0, run_to = 0;  // stage range of the last run_stages (bgv_last_stats)
   dev_batch last_d = {};         // the last run_stages batch (its pipeline variant for bgv_stats)
   hipStream_t st = nullptr, st_hash = nullptr, st_pk = nullptr;
+  hipStream_t st_chk = nullptr;  // deferred subgroup checks, low priority (BGV_CHK_STREAM)
   hipEvent_t ev[ST_COUNT + 1] = {};   // ev[s] = start of stage s on its stream
   hipEvent_t ev_end[ST_COUNT] = {};   // end of stage s on its stream
   hipEvent_t ev_fork = nullptr;
@@ -74,6 +75,7 @@ struct bgv_ctx {
   hipEvent_t ev_sigdec = nullptr;     // defer_grp: signatures decoded (the checks may start)
   hipEvent_t ev_grp = nullptr;        // defer_grp: subgroup checks done (the code fix-up may start)
   hipEvent_t ev_maps = nullptr;       // early_maps: the hash maps on st_hash are done
+  hipEvent_t ev_chk = nullptr;        // pubkey scaling done: the deferred checks may start on st_chk
   hipEvent_t ev_dep[ST_COUNT] = {};   // untimed cross-stream dependencies (latency batches)
   // index2pubkey table (grown by copy) and synthetic secret keys
   g1a* table = nullptr;
@@ -214,6 +216,7 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
   HIPCHK(hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, prio_lo));
   HIPCHK(hipStreamCreateWithPriority(&c->st_hash, hipStreamNonBlocking, prio_hi));
   HIPCHK(hipStreamCreateWithPriority(&c->st_pk, hipStreamNonBlocking, prio_hi));
+  HIPCHK(hipStreamCreateWithPriority(&c->st_chk, hipStreamNonBlocking, prio_lo));
   for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
   for (auto& e : c->ev_end) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipEventCreate(&c->ev_fork));
@@ -223,6 +226,7 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
   HIPCHK(hipEventCreateWithFlags(&c->ev_sigdec, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&c->ev_grp, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&c->ev_maps, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&c->ev_chk, hipEventDisableTiming));
   *out = c;
   return BGV_OK;
 }
@@ -233,6 +237,7 @@ int bgv_close(bgv_ctx* c) {
   (void)hipStreamSynchronize(c->st);
   (void)hipStreamSynchronize(c->st_hash);
   (void)hipStreamSynchronize(c->st_pk);
+  (void)hipStreamSynchronize(c->st_chk);
   for (auto& e : c->ev) (void)hipEventDestroy(e);
   for (auto& e : c->ev_end) (void)hipEventDestroy(e);
   (void)hipEventDestroy(c->ev_fork);
@@ -242,6 +247,7 @@ int bgv_close(bgv_ctx* c) {
   (void)hipEventDestroy(c->ev_sigdec);
   (void)hipEventDestroy(c->ev_grp);
   (void)hipEventDestroy(c->ev_maps);
+  (void)hipEventDestroy(c->ev_chk);
   if (c->pin_in) (void)hipHostFree(c->pin_in);
   if (c->pin_out) (void)hipHostFree(c->pin_out);
   if (c->table) (void)hipFree(c->table);
@@ -259,6 +265,7 @@ int bgv_close(bgv_ctx* c) {
   (void)hipStreamDestroy(c->st);
   (void)hipStreamDestroy(c->st_hash);
   (void)hipStreamDestroy(c->st_pk);
+  (void)hipStreamDestroy(c->st_chk);
   delete c;
   return BGV_OK;
 }
@@ -417,6 +424,9 @@ static bool layout_split(const bgv_cfg& k, uint32_t n) { return k.split >= 0 ? k
 // before the host reads back offsets, checks them and sets up the rest
 // (on-device batches: ~0.1 ms of idle GPU at 3,136 sets, r04c timeline).
 // Timed runs keep the maps inside the hash stage's events.
+#ifndef BGV_CHK_STREAM
+#define BGV_CHK_STREAM 1
+#endif
 #ifndef BGV_EARLY_MAPS
 #define BGV_EARLY_MAPS 1
 #endif
@@ -759,12 +769,20 @@ static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int fro
     else if (fork && (s == ST_PK_SCALE || s == ST_HASH || s == ST_MILLER)) HIPCHK(hipEventRecord(c->ev_dep[s], st));
     if (d.defer_grp && s == ST_SIG && fork) HIPCHK(hipEventRecord(c->ev_sigdec, st));
     if (d.defer_grp && s == ST_PK_SCALE) {
-      // the pubkey stream is idle once the Miller loops have their keys: the
-      // checks run there, beside them (the Miller loops wait on the event above)
-      if (fork) HIPCHK(hipStreamWaitEvent(st, c->ev_sigdec, 0));
-      launch_sig_check(st, d, w);
+      // the checks start once the Miller loops have their keys, beside them;
+      // BGV_CHK_STREAM: on a low-priority stream of their own, so the waves of
+      // the hash stream (the fixed-argument lines, then the Miller loops) are
+      // dispatched first when slots free up
+      hipStream_t cs = st;
+      if (fork && BGV_CHK_STREAM) {
+        HIPCHK(hipEventRecord(c->ev_chk, st));
+        cs = c->st_chk;
+        HIPCHK(hipStreamWaitEvent(cs, c->ev_chk, 0));
+      }
+      if (fork) HIPCHK(hipStreamWaitEvent(cs, c->ev_sigdec, 0));
+      launch_sig_check(cs, d, w);
       HIPCHK(hipGetLastError());
-      if (fork) HIPCHK(hipEventRecord(c->ev_grp, st));
+      if (fork) HIPCHK(hipEventRecord(c->ev_grp, cs));
     }
     return 0;
   };
