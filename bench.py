@@ -443,9 +443,11 @@ def main():
     from lodestar_amd import native
     from lodestar_amd.dist import batch_job_work, gather_job_results, select_jobs, shard_jobs, verify_sharded
 
-    # per-stage timing events: automatic from 65,536 sets; forced for the
-    # smaller shards of N > 1 (they would add queue time to the N = 1 latency legs)
-    d = native.Device(gpu, timing=1) if world > 1 else native.Device(gpu)
+    # per-stage timing events are automatic from 65,536 sets; below that they
+    # add ~5 us of queue time per event on the critical path (C4/8 shard 9.65 ->
+    # 9.75 ms, profiles/r04g_sweep_timed.txt), so the timed steps of N > 1 run
+    # without them and one extra step on a timed context gives the breakdown
+    d = native.Device(gpu)
     t0 = time.time()
     d.gen_keys(0, N_VALIDATORS, SEED)
     log(f"[bench] {N_VALIDATORS} keys generated in {time.time() - t0:.1f}s")
@@ -504,8 +506,14 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = total_sets * args.steps / elapsed
 
-    stage_ms = {d.stage_name(i): float(stage_sum[i] / args.steps) for i in range(native.N_STAGES) if d.stage_name(i) != "unknown"}
     timed_layout = d.last_stats.layout()  # the variant the timed batches ran with (bgv_stats), before the extra legs
+    if not stage_sum.any():  # untimed shard steps: one step of the same shard on a timed context, after the timed region
+        dt = native.Device(gpu, timing=1)
+        dt.gen_keys(0, N_VALIDATORS, SEED)
+        dt.partial(darr, on_device=True)
+        stage_sum = np.array(list(dt.last_stats.stage_ms)) * args.steps
+        dt.close()
+    stage_ms = {d.stage_name(i): float(stage_sum[i] / args.steps) for i in range(native.N_STAGES) if d.stage_name(i) != "unknown"}
 
     legs = {}
     if shard and not args.no_weak_leg:
