@@ -134,7 +134,15 @@ BGV_NIS void miller_add_step(g2p_t& T, fp2_t& a0, fp2_t& a1, fp2_t& b1, const g2
 // lines[(3 step + c) stride + i]; miller_line_at_p finishes one at P with
 // the operations the steps above apply, so f is bit-identical.
 constexpr int MILLER_STEPS = 68;
-BGV_NI void miller_lines(fp2_t* lines, uint32_t stride, uint32_t i, const g2a& Q) {
+#ifndef BGV_LINES_INLINE
+#define BGV_LINES_INLINE 1  // into k_lines: scratch 960 -> 496 B/lane (r04)
+#endif
+#if BGV_LINES_INLINE
+BGV_HD
+#else
+BGV_NI
+#endif
+void miller_lines(fp2_t* lines, uint32_t stride, uint32_t i, const g2a& Q) {
   g2p_t T;
   T.x = Q.x;
   T.y = Q.y;
