@@ -305,6 +305,31 @@ def small_configs(d, torch, dev, arrays):
     return out
 
 
+def mixed_sizes(d, darr, reps: int = 4):
+    """A node alternating gossip batches with range-sync segments:
+    C2 (64 sets, host-resident, no fixed-argument lines) then the device-resident
+    C4 segment (lines), `reps` times.  The line buffer stays allocated across the
+    small batches (bgv_api.hip LINES_KEEP), so the C4 calls of the mixed
+    sequence take what the plain ones do."""
+    g = build_segment([0], seed=SEED + 1000)
+    n2, k2 = 64, ATT_K
+    c2a = signed(d, {"n_sets": n2, "n_jobs": 1, "job_offsets": np.array([0, n2], np.uint32),
+                     "pk_offsets": (np.arange(n2 + 1) * k2).astype(np.uint32),
+                     "pk_indices": g["pk_indices"][: n2 * k2].copy(), "msgs": g["msgs"][:n2].copy(), "n_raw": 0})
+    c2_ms, c4_ms = [], []
+    for _ in range(reps):
+        t1 = time.perf_counter()
+        jr, _ = d.verify(c2a, want_set_codes=False)
+        c2_ms.append((time.perf_counter() - t1) * 1e3)
+        assert (jr == 1).all()
+        t1 = time.perf_counter()
+        jr, _ = d.verify(darr, on_device=True, want_set_codes=False)
+        c4_ms.append((time.perf_counter() - t1) * 1e3)
+        assert (jr == 1).all()
+    return {"c2_ms_p50": round(float(np.median(c2_ms)), 3), "c4_ms_p50": round(float(np.median(c4_ms)), 3),
+            "reps": reps, "note": "C2 and C4 batches alternated on one context"}
+
+
 def epoch_slice(d, torch, dev, arrays_host: dict, sigs, blocks: int = 32, reps: int = 7):
     """One epoch of the segment (32 blocks = 3,136 sets): the batch a range
     sync hands the verifier per epoch (sync/constants.ts:41), on device, p50"""
@@ -526,6 +551,7 @@ def main():
         host["scalars"] = None
         legs["c4_host_resident"] = host_resident_c4(d, host)
         legs["c4_epoch_slice"] = epoch_slice(d, torch, dev, arrays, host["sigs"])
+        legs["mixed_sizes"] = mixed_sizes(d, darr)
         if world == 1:
             legs["strong_shard_projection"] = shard_projection(d, torch, dev, host)
 

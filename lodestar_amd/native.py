@@ -251,9 +251,12 @@ def _sync_producers(*objs) -> None:
             if a is None or isinstance(a, (np.ndarray, bytes, bytearray, int, float, str)):
                 continue
             dev = getattr(a, "device", None)
-            if dev is None or getattr(dev, "type", "") != "cuda" or dev in seen:
+            if dev is None or getattr(dev, "type", "") != "cuda":
                 continue
-            seen.add(dev)
+            key = getattr(dev, "index", None)
+            if key in seen:
+                continue
+            seen.add(key)
             import torch
             torch.cuda.current_stream(dev).synchronize()
 

@@ -156,3 +156,35 @@ def test_stale_library_refuses_to_load(lib, tmp_path):
     env.pop("BGV_LIB", None)
     out = subprocess.check_output([__import__("sys").executable, "-c", code], env=env).decode()
     assert out.startswith("refused") and "other sources" in out
+
+
+def test_device_inputs_wait_for_their_producing_stream(monkeypatch):
+    """native._sync_producers: one current-stream synchronize per CUDA device a
+    tensor argument lives on; numpy arrays, None and scalars need none"""
+    import types
+
+    import numpy as np
+    import torch
+
+    from lodestar_amd import native
+    calls = []
+
+    class _Stream:
+        def __init__(self, dev):
+            self.dev = dev
+
+        def synchronize(self):
+            calls.append(self.dev)
+
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda dev=None: _Stream(dev))
+    d0 = types.SimpleNamespace(type="cuda", index=0)
+    d1 = types.SimpleNamespace(type="cuda", index=1)
+    cpu = types.SimpleNamespace(type="cpu", index=None)
+    t = lambda dev: types.SimpleNamespace(device=dev, data_ptr=lambda: 0)
+    native._sync_producers({"a": np.zeros(3), "b": None, "n": 5, "c": t(d0), "d": t(d0), "e": t(d1), "f": t(cpu)})
+    assert calls == [d0, d1]
+    calls.clear()
+    native._sync_producers({"a": np.zeros(3)}, None)
+    assert calls == []
+    native._sync_producers(t(d1))
+    assert calls == [d1]
