@@ -773,8 +773,10 @@ static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int fro
       // BGV_CHK_STREAM: on a low-priority stream of their own, so the waves of
       // the hash stream (the fixed-argument lines, then the Miller loops) are
       // dispatched first when slots free up
+      // (latency-mode batches only: at C4 the checks on the pubkey stream measured
+      // 0.3 ms faster, 4 same-box rounds, profiles/r04z_ab_chk_c4.txt)
       hipStream_t cs = st;
-      if (fork && BGV_CHK_STREAM) {
+      if (fork && BGV_CHK_STREAM && d.split) {
         HIPCHK(hipEventRecord(c->ev_chk, st));
         cs = c->st_chk;
         HIPCHK(hipStreamWaitEvent(cs, c->ev_chk, 0));

@@ -3,7 +3,7 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out; rm -f gpurun_out/ab.txt
-for rep in 1 2 3; do LIBS="$LIBS" SIZES=${SIZES:-100352} bash tools/ab_lib.sh; done
+for rep in ${ROUNDS:-1 2 3}; do LIBS="$LIBS" SIZES=${SIZES:-100352} bash tools/ab_lib.sh; done
 python3 - <<'PY'
 import json, collections
 r = collections.defaultdict(list)
