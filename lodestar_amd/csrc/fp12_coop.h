@@ -34,6 +34,9 @@ struct cscratch {
 #ifndef BGV_COOP_TREE
 #define BGV_COOP_TREE 1  // c_mul2: the output sums across lanes instead of a third round
 #endif
+#ifndef BGV_CMUL_ADDR
+#define BGV_CMUL_ADDR 1
+#endif
 #if BGV_COOP_LDS_AS && BGV_COOP_TREE
 // out = a * b in TWO rounds: the 108 Fp products, then one Fp component per
 // lane (wave c = component c): lane m = 6k + i takes the product pair
@@ -55,6 +58,21 @@ __device__ void c_mul(wfp12* out_, const wfp12* a_, const wfp12* b_, cscratch* s
   if (l < 108) {
     const uint32_t p = l / 3, q = l - 3 * p, i = p / 6, j = p - 6 * i;
     fp_t u, v;
+#if BGV_CMUL_ADDR
+    // operands by address, not by value selects: component q (q < 2) or c0,
+    // plus c1 masked in for the Karatsuba sum (q = 2; a lazy sum of x and 0
+    // is x), so every lane runs one load pair and one lazy addition
+    const uint32_t m = q == 2 ? ~0u : 0u;
+    const fp_t xa = lds_get(q == 1 ? &a->c[i].c1 : &a->c[i].c0), ya = lds_get(&a->c[i].c1);
+    const fp_t xb = lds_get(q == 1 ? &b->c[j].c1 : &b->c[j].c0), yb = lds_get(&b->c[j].c1);
+    fp_t ma, mb;
+#pragma unroll
+    for (int k = 0; k < NL; k++) {
+      ma.l[k] = ya.l[k] & m;
+      mb.l[k] = yb.l[k] & m;
+    }
+    fp_add_lazy2(u, xa, ma, v, xb, mb);
+#else
     if (q == 0) {
       u = lds_get(&a->c[i].c0);
       v = lds_get(&b->c[j].c0);
@@ -64,6 +82,7 @@ __device__ void c_mul(wfp12* out_, const wfp12* a_, const wfp12* b_, cscratch* s
     } else {
       fp_add_lazy2(u, lds_get(&a->c[i].c0), lds_get(&a->c[i].c1), v, lds_get(&b->c[j].c0), lds_get(&b->c[j].c1));
     }
+#endif
     fp_t r;
     fp_mul(r, u, v);
     lds_put(&s->p[l], r);
@@ -79,17 +98,32 @@ __device__ void c_mul(wfp12* out_, const wfp12* a_, const wfp12* b_, cscratch* s
     const uint32_t comp = l >> 6, m = l & 63u;
     const uint32_t k = m / 6 < 6 ? m / 6 : 0u, i = m % 6, j = (k + 6 - i) % 6, pr = i * 6 + j;
     const bool xi = i + j >= 6;
-    const fp_t p0 = lds_get(&s->p[3 * pr]), p1 = lds_get(&s->p[3 * pr + 1]), p2 = lds_get(&s->p[3 * pr + 2]);
-    fp_t zero;
-    fp_set_zero(zero);
     // w = a + b;  t = c - d
     //   re, no xi: (P0 + 0) - P1     re, xi: (P0 + P0) - P2
     //   im, no xi: P2 - (P0 + P1)    im, xi: P2 - (P1 + P1)
+#if BGV_CMUL_ADDR
+    // a, b and the other term Q by address (b masked to 0 for re without xi):
+    // re: t = w - Q, im: t = Q - w
+    const uint32_t mb = comp || xi ? ~0u : 0u;
+    const fp_t a = lds_get(&s->p[3 * pr + (comp && xi ? 1u : 0u)]);
+    const fp_t b0 = lds_get(&s->p[3 * pr + (comp ? 1u : 0u)]);
+    const fp_t Q = lds_get(&s->p[3 * pr + (comp || xi ? 2u : 1u)]);
+    fp_t b;
+#pragma unroll
+    for (int k = 0; k < NL; k++) b.l[k] = b0.l[k] & mb;
+    fp_t w, t;
+    fp_add(w, a, b);
+    fp_sub(t, comp ? Q : w, comp ? w : Q);
+#else
+    const fp_t p0 = lds_get(&s->p[3 * pr]), p1 = lds_get(&s->p[3 * pr + 1]), p2 = lds_get(&s->p[3 * pr + 2]);
+    fp_t zero;
+    fp_set_zero(zero);
     const fp_t& a = comp ? (xi ? p1 : p0) : p0;
     const fp_t& b = comp ? p1 : (xi ? p0 : zero);
     fp_t w, t;
     fp_add(w, a, b);
     fp_sub(t, comp ? p2 : w, comp ? w : (xi ? p2 : p1));
+#endif
     const uint32_t src1 = m + 1 < 64 ? l + 1 : l, src2 = m + 2 < 64 ? l + 2 : l, src4 = m + 4 < 64 ? l + 4 : l;
     fp_t x = c_pull1(t, src1 & 63u);  // i even: t_i + t_(i+1)
     fp_add(t, t, x);
