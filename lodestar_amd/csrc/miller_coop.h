@@ -109,8 +109,26 @@ __device__ __forceinline__ void coop_wave_sync() { __asm__ volatile("s_waitcnt l
 // q2 (a0 + a1)(b0 + b1) (one leaf call on every lane), then q0 / q1 form
 // c0 = P0 - P1 / c1 = P2 - P0 - P1.  All three sub-lanes of k call it
 // together (the branch conditions around every call depend on k only).
+#ifndef BGV_CPROD_ADDR
+#define BGV_CPROD_ADDR 1  // operands by address + a masked lazy sum, no divergent 3-way branch
+#endif
 __device__ __forceinline__ void coop_prod_sub(fp_t* P, uint32_t q, const fp2_t* a, const fp2_t* b, fp2_t* out) {
   fp_t u, v;
+#if BGV_CPROD_ADDR
+  {
+    // sub-lane q: component q (q < 2) or c0 + c1 (q = 2: c1 masked in; a lazy
+    // sum of x and 0 is x)
+    const uint32_t m = q == 2 ? ~0u : 0u;
+    const fp_t xa = *(q == 1 ? &a->c1 : &a->c0), xb = *(q == 1 ? &b->c1 : &b->c0);
+    fp_t ma, mb;
+#pragma unroll
+    for (int k = 0; k < NL; k++) {
+      ma.l[k] = a->c1.l[k] & m;
+      mb.l[k] = b->c1.l[k] & m;
+    }
+    fp_add_lazy2(u, xa, ma, v, xb, mb);  // < 2p, product inputs only
+  }
+#else
   if (q == 0) {
     u = a->c0;
     v = b->c0;
@@ -121,6 +139,7 @@ __device__ __forceinline__ void coop_prod_sub(fp_t* P, uint32_t q, const fp2_t* 
     fp_add_lazy(u, a->c0, a->c1);  // < 2p, product inputs only
     fp_add_lazy(v, b->c0, b->c1);
   }
+#endif
   fp_t r;
   fp_mul(r, u, v);
   P[q] = r;
