@@ -548,15 +548,18 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   //    the latency-mode hash (two-lane maps, one-lane clearing) with the
   //    one-lane Miller loop and the (job, window) MSM up to 65,536 sets
   //    (37,632: 25.1 -> 22.5 ms; 50,176: 26.0 -> 24.9 ms)
-  static const uint32_t MILLER18_MIN = 2000, MILLER4_MIN = 6000, MILLER2_MIN = 18000, MILLER1_MIN = 35000,
+  static const uint32_t MILLER18_MIN = 2000, MILLER4_MIN = 6000, MILLER2_MIN = 15000, MILLER1_MIN = 35000, CLEAR1_MIN = 16500,
                         MSM_MIN = 6000, MSM4_MIN = 9000, MSM2_MIN = 35000, PAIRS2_MIN = 65536,
                         CLEAR3_MIN = 9000, KV6_MIN = 1100, KV3_MIN = 4500, KV_MAX = 11500;
   const bgv_cfg& k = c->cfg;
   d.pairs_per_item = k.pairs ? (uint32_t)k.pairs : (n >= PAIRS2_MIN ? 2u : 1u);
   d.split = layout_split(k, n) ? 1u : 0u;
-  // one lane per point from 18,000 sets (25,088: 16.74 -> 16.5 ms; the trio's
-  // 1,176 waves oversubscribe the SIMDs there)
-  d.clear_lanes = k.clear_lanes > 0 ? (uint32_t)k.clear_lanes : (n < CLEAR3_MIN ? 9u : n < MILLER2_MIN ? 3u : 1u);
+  // one lane per point from 16,500 sets (25,088: 16.74 -> 16.5 ms; 17,248:
+  // 14.24 -> 13.95 ms; the trio's waves oversubscribe the SIMDs there) and the
+  // two-lane Miller loop from 15,000 (r04 sweep, profiles/r04z_sweep_cliff.txt:
+  // the four-lane loop's waves oversubscribe from ~15,000 sets: 15,680 sets
+  // 12.38 -> 12.10 ms, 17,248 sets 16.61 -> 13.95 ms)
+  d.clear_lanes = k.clear_lanes > 0 ? (uint32_t)k.clear_lanes : (n < CLEAR3_MIN ? 9u : n < CLEAR1_MIN ? 3u : 1u);
   // sum r_i sigma_i per job by a bucket MSM (16 x 4-bit windows) when jobs
   // are block-sized (<= 256 sets).  The latency mode takes the fused kernel
   // (one workgroup per job, k_msm_fused: short chain, many idle lanes); bulk
