@@ -415,7 +415,7 @@ static int stage_issue(bgv_ctx* c, size_t total) {
 
 // latency mode by batch size (prepare(); the r02 sweep: 25,088 sets 24.5 ms
 // split against 26.3 ms, 50,176: 35.4 against 29.3; r03: to 65,536)
-static const uint32_t SPLIT_MAX = 60000;
+static const uint32_t SPLIT_MAX = 59000;
 static bool layout_split(const bgv_cfg& k, uint32_t n) { return k.split >= 0 ? k.split != 0 : n < SPLIT_MAX; }
 
 // The hash maps of a latency-mode batch read only the messages, and they head
@@ -550,8 +550,9 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   //    (37,632: 25.1 -> 22.5 ms; 50,176: 26.0 -> 24.9 ms)
   //  * r04 sweeps: the one-lane Miller loop and the (job, window) MSM from
   //    32,000 sets (32,928 / 34,496 sets 25.1 / 25.3 -> 22.0 / 22.1 ms), the
-  //    bulk kernels from 60,000 (62,720 sets 32.1 -> 30.3 ms;
-  //    profiles/r04z_sweep_big.txt)
+  //    bulk kernels from 59,000 (62,720 sets 32.1 -> 30.3 ms, 59,584 sets
+  //    30.5 -> 28.0 ms; 58,016 sets stay split: 27.1 against 28.7 ms;
+  //    profiles/r04z_sweep_big.txt, profiles/r04z_sweep_split_edge.txt)
   static const uint32_t MILLER18_MIN = 2000, MILLER4_MIN = 6000, MILLER2_MIN = 15000, MILLER1_MIN = 32000, CLEAR1_MIN = 16500,
                         MSM_MIN = 6000, MSM4_MIN = 9000, MSM2_MIN = 32000, PAIRS2_MIN = 65536,
                         CLEAR3_MIN = 9000, KV6_MIN = 1100, KV3_MIN = 4500, KV_MAX = 11500;

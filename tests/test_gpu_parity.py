@@ -399,7 +399,7 @@ def test_signature_tree_large_jobs_bit_identical():
 
 @pytest.mark.gpu
 def test_latency_split_mode_bit_identical():
-    """Latency mode (bgv_cfg.split = 1, default below 60,000 sets: two map lanes
+    """Latency mode (bgv_cfg.split = 1, default below 59,000 sets: two map lanes
     per message, subgroup check beside [r_i] sigma_i) and the one-lane-per-set
     kernels (split = 0) give the same batch partial, byte for byte, and the
     same per-job verdicts and set codes on the golden jobs (which include
