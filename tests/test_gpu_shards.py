@@ -8,6 +8,11 @@ pipeline layouts (no bgv_cfg overrides), through both device paths:
     sync/constants.ts:41; two-pair view Miller loop on 18 lanes, nine-lane
     view clearing), and the two other view-Miller ranges: 16 blocks = 1,568
     sets (18 lanes per two pairs) and 64 blocks = 6,272 sets (9 lanes),
+  * the layouts of the larger shards (fewer GPUs, or one GPU taking a bigger
+    share): 256 blocks = 25,088 sets = C4/4 (two-lane Miller loop, digit MSM),
+    352 blocks = 34,496 sets (one-lane Miller loop and (job, window) MSM in
+    latency mode, from 32,000 sets) and 608 blocks = 59,584 sets (bulk hash,
+    one pair per Miller item, from 59,000 sets),
 
 each with 1 % faults of the four C5 kinds (bench.inject_faults: wrong message,
 swapped pubkey, cleared compression flag, on-curve point outside G2):
@@ -47,7 +52,12 @@ def dev():
 
 
 # blocks -> the layout prepare() picks by default at that size (bgv_api.hip)
-SIZES = {128: "c4_over_8", 64: "view_miller_9_lanes", 32: "epoch_slice", 16: "view_miller_18_lanes"}
+SIZES = {128: "c4_over_8", 64: "view_miller_9_lanes", 32: "epoch_slice", 16: "view_miller_18_lanes",
+         256: "c4_over_4", 352: "one_lane_miller_latency_hash", 608: "bulk_one_pair_per_item"}
+# the layout fields prepare() must pick at the larger sizes (bgv_api.hip thresholds)
+LAYOUT = {256: {"split": 1, "miller_lanes": 2, "msm": 4, "clear_lanes": 1},
+          352: {"split": 1, "miller_lanes": 1, "msm": 2, "clear_lanes": 1},
+          608: {"split": 0, "miller_lanes": 1, "pairs_per_item": 1, "msm": 2}}
 
 
 @pytest.mark.parametrize("blocks", sorted(SIZES))
@@ -66,6 +76,8 @@ def test_faulted_shard_default_layout(dev, blocks):
     assert sc.tolist() == code.tolist()
     assert dev.last_stats.batch_retries == 1
     print(f"{n} sets, default layout {layout}")
+    for k, v in LAYOUT.get(blocks, {}).items():
+        assert layout[k] == v, (k, layout)
 
     # 2a. the whole batch as one shard: partial -> combined check -> localisation
     part, sc2, prov, ok = dev.partial(fa)
