@@ -364,6 +364,19 @@ static void random_bytes(void* out, size_t n) {
   }
 }
 
+// a device allocation of prepare(): under memory pressure a kept line buffer
+// (up to 2.6 GB, see work_alloc) gives way first, then the allocation retries
+template <class T>
+static int ensure_or_release_lines(bgv_ctx* c, dbuf<T>& b, size_t n) {
+  int r = b.ensure(n);
+  if (r && c->lines.cap && (const void*)&b != (const void*)&c->lines) {
+    c->lines.release();
+    c->lines_idle = 0;
+    r = b.ensure(n);
+  }
+  return r;
+}
+
 static int pinned_reserve(uint8_t*& p, size_t& cap, size_t n) {
   if (n <= cap) return 0;
   size_t c = cap ? cap : 65536;
@@ -394,7 +407,7 @@ static int stage_pack(bgv_ctx* c, stage_seg* segs, int n_segs, size_t& total) {
     c->staged_pending = false;
   }
   if (int r = pinned_reserve(c->pin_in, c->pin_in_cap, total ? total : 1)) return r;
-  if (int r = c->stage_dev.ensure(total ? total : 1)) return r;
+  if (int r = ensure_or_release_lines(c, c->stage_dev, total ? total : 1)) return r;
   size_t off = 0;
   for (int i = 0; i < n_segs; i++) {
     if (segs[i].bytes) memcpy(c->pin_in + off, segs[i].src, segs[i].bytes);
@@ -435,11 +448,14 @@ static int early_maps(bgv_ctx* c, dev_batch& d, bool after_staging) {
   if (!BGV_EARLY_MAPS) return 0;
   const bool timed = c->cfg.timing >= 0 ? c->cfg.timing != 0 : n >= 65536;
   if (!n || timed || !layout_split(c->cfg, n)) return 0;
-  if (int r = c->q_part.ensure(2 * (size_t)n)) return r;
+  if (int r = ensure_or_release_lines(c, c->q_part, 2 * (size_t)n)) return r;
   if (after_staging) HIPCHK(hipStreamWaitEvent(c->st_hash, c->ev_staged, 0));
   dev_work w;
   memset(&w, 0, sizeof w);
   w.q_part = c->q_part.p;
+  // the batch's start event goes in front of the maps (they head the critical
+  // path), so stats total_ms covers them; run_stages then does not re-record it
+  HIPCHK(hipEventRecord(c->ev[0], c->st_hash));
   launch_hash_maps(c->st_hash, d, w);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev_maps, c->st_hash));
@@ -505,7 +521,7 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
       if (int r = early_maps(c, d, true)) return r;
     if (!b->scalars) d.scalars = nullptr;
     if (!need_sigs) { d.sigs = nullptr; d.sig_len = nullptr; }
-    if (int r = c->raw_conv.ensure(b->n_raw ? b->n_raw : 1)) return r;
+    if (int r = ensure_or_release_lines(c, c->raw_conv, b->n_raw ? b->n_raw : 1)) return r;
     launch_raw_pks(c->st, raw_dev, c->raw_conv.p, b->n_raw);
     d.raw_pks = c->raw_conv.p;
   } else {
@@ -517,7 +533,7 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
     d.sig_len = b->sig_len;
     if (need_sigs)
       if (int r = early_maps(c, d, false)) return r;
-    if (int r = c->raw_conv.ensure(b->n_raw ? b->n_raw : 1)) return r;
+    if (int r = ensure_or_release_lines(c, c->raw_conv, b->n_raw ? b->n_raw : 1)) return r;
     launch_raw_pks(c->st, b->raw_pks, c->raw_conv.p, b->n_raw);
     d.raw_pks = c->raw_conv.p;
     // offsets live in HBM: the host needs the job offsets (stats) and the key total (grid bound)
@@ -647,7 +663,7 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
     // getrandom() (+ 12-byte nonce) per call, rng.h
     uint32_t kn[11];
     random_bytes(kn, sizeof kn);
-    if (int r = c->scalars.ensure(n ? n : 1)) return r;
+    if (int r = ensure_or_release_lines(c, c->scalars, n ? n : 1)) return r;
     launch_gen_scalars(c->st, kn, kn + 8, c->scalars.p, n);
     HIPCHK(hipGetLastError());
     d.scalars = c->scalars.p;
@@ -742,7 +758,7 @@ static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int fro
   c->run_from = from;
   c->run_to = to;
   hipEvent_t* dep = timed ? c->ev_end : c->ev_dep;  // what the stream waits below wait on
-  if (!timed) HIPCHK(hipEventRecord(c->ev[from], c->st));
+  if (!timed && !(d.maps_early && from == 0)) HIPCHK(hipEventRecord(c->ev[from], c->st));
   // latency batches fork the hash leg BEFORE the index set-up: hash_to_G2 reads
   // only the messages and heads the critical path (hash -> Miller -> fold ->
   // final exp); large batches keep the set-up alone on the GPU (its

@@ -161,6 +161,7 @@ __global__ void __launch_bounds__(64, 1) k_miller_kv(dev_batch b, dev_work w) {
   __shared__ mkv_scratch sm[G + 1];
   const uint32_t lane = threadIdx.x, grp = lane / LANES, r = lane % LANES, s = r / 3u, q = r % 3u;
   const uint32_t n_items = w.item_off[b.n_jobs];
+  if (n_items == 0) return;  // wave-uniform: a batch of empty jobs has no item (item_job[0] is stale)
   const uint32_t t0 = blockIdx.x * G + grp;
   const bool own = grp < (uint32_t)G && t0 < n_items;
   const uint32_t t = own ? t0 : 0u;
@@ -222,7 +223,7 @@ __global__ void __launch_bounds__(64, 1) k_miller_kv(dev_batch b, dev_work w) {
 void launch_miller_kv(hipStream_t st, const dev_batch& b, const dev_work& w) {
   // items <= n_sets / 2 + n_jobs (a job of odd size leaves a one-pair item)
   const uint32_t items = b.n_sets / 2u + b.n_jobs;
-  if (!items) return;
+  if (!items || !b.n_sets) return;
   if (b.miller_kv == 9) {
     constexpr uint32_t G = 64 / 27;
     hipLaunchKernelGGL(k_miller_kv<9>, dim3((items + G - 1) / G), dim3(64), 0, st, b, w);

@@ -31,7 +31,8 @@ const path = require("path");
 // starts: in a host that has already done fs / crypto work (Lodestar has) this
 // default is ignored, so the launcher sets it before Node starts
 // (INTEGRATION.md section 4) and the constructor warns when it is too small.
-if (!process.env.UV_THREADPOOL_SIZE) process.env.UV_THREADPOOL_SIZE = "16";
+const UV_POOL_PRESET = process.env.UV_THREADPOOL_SIZE;
+if (!UV_POOL_PRESET) process.env.UV_THREADPOOL_SIZE = "16";
 
 const addon = require(path.join(__dirname, "bgv.node"));
 
@@ -55,8 +56,16 @@ function sourceHash(root = path.join(__dirname, "..", "..")) {
   return h.digest("hex");
 }
 
+// an install that ships bgv.node + libbgv.so without the csrc tree cannot be
+// compared: the check is skipped with a warning (INTEGRATION.md section 3)
 function checkBuildId(id = addon.buildId()) {
-  const want = sourceHash();
+  let want;
+  try {
+    want = sourceHash();
+  } catch (e) {
+    console.warn(`BlsGpuVerifier: libbgv.so build id not checked (sources not readable: ${e.message})`);
+    return;
+  }
   if (id !== want && !id.startsWith(want + "+")) {
     throw Error(`libbgv.so was built from other sources (id ${id.slice(0, 16)}, tree ${want.slice(0, 16)}): rebuild`);
   }
@@ -224,9 +233,13 @@ class BlsGpuVerifier {
     // every device batch holds a libuv pool thread (napi_async_work); the pool
     // size is read once, when the pool first starts, so the launcher must set
     // UV_THREADPOOL_SIZE before Node runs any async work (INTEGRATION.md 4)
-    const pool = Number(process.env.UV_THREADPOOL_SIZE) || 4;
+    // UV_THREADPOOL_SIZE; judged on the value the process started with: the
+    // 16 this module assigns when it was unset only counts if the pool had
+    // not started yet, which the module cannot tell, so it assumes libuv's 4
+    const pool = Number(UV_POOL_PRESET) || 4;
     if (ids.length + 2 > pool) {
-      console.warn(`BlsGpuVerifier: ${ids.length} devices with UV_THREADPOOL_SIZE=${pool}: device batches will ` +
+      const was = UV_POOL_PRESET ? `UV_THREADPOOL_SIZE=${pool}` : "UV_THREADPOOL_SIZE unset at start (libuv default 4)";
+      console.warn(`BlsGpuVerifier: ${ids.length} devices with ${was}: device batches may ` +
         "serialise and starve other pool work; start Node with UV_THREADPOOL_SIZE >= devices + 2");
     }
     this.ctxs = ids.map((d) => addon.open(d));

@@ -169,8 +169,15 @@ def source_hash(root: str = ROOT) -> str:
 
 def check_build_id(lib_id: str, root: str = ROOT) -> None:
     """A library compiled from other sources than the tree beside it is
-    refused (variant builds carry the id plus '+' and their defines)."""
-    want = source_hash(root)
+    refused (variant builds carry the id plus '+' and their defines).  An
+    install that ships the library without its csrc tree has nothing to
+    compare against: the check is skipped with a warning."""
+    try:
+        want = source_hash(root)
+    except OSError as e:
+        import warnings
+        warnings.warn(f"libbgv.so build id not checked: sources not readable ({e})", RuntimeWarning, stacklevel=2)
+        return
     if lib_id != want and not lib_id.startswith(want + "+"):
         raise BgvNativeError(BGV_E_INVALID_ARG,
                              f"libbgv.so was built from other sources (id {lib_id[:16]}, tree {want[:16]}): "
@@ -186,10 +193,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
             return _lib
         if not os.path.exists(path):
             raise BgvNativeError(BGV_E_NO_DEVICE, f"{path} not built (run __graft_entry__.build())")
-        lib = ctypes.CDLL(path)
-        lib.bgv_build_id.argtypes = []
-        lib.bgv_build_id.restype = ctypes.c_char_p
-        check_build_id(lib.bgv_build_id().decode())
+        try:
+            lib = ctypes.CDLL(path)
+            build_id_fn = lib.bgv_build_id
+        except (OSError, AttributeError) as e:
+            raise BgvNativeError(BGV_E_INVALID_ARG, f"{path}: not a loadable libbgv.so of this ABI ({e}): rebuild") from e
+        build_id_fn.argtypes = []
+        build_id_fn.restype = ctypes.c_char_p
+        check_build_id(build_id_fn().decode())
         P = ctypes.c_void_p
         u32, i32, u64 = ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64
         sig = {

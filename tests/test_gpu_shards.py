@@ -28,7 +28,9 @@ swapped pubkey, cleared compression flag, on-curve point outside G2):
 
 and the real partial path over two ranks: two processes, one context each
 (both on GPU 0), gloo all-gathers of the 576-byte partials and of the per-job
-verdicts (lodestar_amd/dist.py verify_sharded / gather_job_results).
+verdicts (lodestar_amd/dist.py verify_sharded / gather_job_results); and the
+same path over an RCCL ("nccl") process group of world size 1 with cuda:0
+tensors, the collective code bench.py takes on the 8-GPU node.
 """
 import os
 import socket
@@ -177,3 +179,62 @@ def test_two_rank_partial_path_gloo():
         assert not valid and full == expect
         valid, full, _ = res[r]["clean"]
         assert valid and full == [1] * BLOCKS_2R
+
+
+def _rccl_rank(port, q):
+    """one rank of an RCCL group (world size 1) on GPU 0: dist.verify_sharded
+    and dist.gather_job_results with device tensors, faulted and clean"""
+    try:
+        import torch
+        import torch.distributed as dist
+
+        from lodestar_amd import native
+        from lodestar_amd.dist import batch_job_work, gather_job_results, select_jobs, shard_jobs, verify_sharded
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        assert dist.get_backend() == "nccl"
+        dev = torch.device("cuda:0")
+        d = native.Device(0)
+        d.gen_keys(0, N_TABLE, SEED)
+        a = bench.build_segment(list(range(BLOCKS_RCCL)), seed=SEED + 7700)
+        fa, expect = bench.inject_faults(d, a, 0.01, SEED + 7800)
+        shards = shard_jobs(batch_job_work(fa), 1)
+        out = {"expect": expect.tolist(), "shard": shards[0]}
+        for name, arr in (("faulted", fa), ("clean", bench.signed(d, a))):
+            jr, _ = d.verify(arr)
+            valid, local = verify_sharded(d, select_jobs(arr, shards[0]), dist, device=dev)
+            full = gather_job_results(local, shards, BLOCKS_RCCL, dist, device=dev)
+            out[name] = (bool(valid), full.tolist(), jr.tolist())
+        d.close()
+        dist.destroy_process_group()
+        q.put(out)
+    except BaseException as e:  # report instead of hanging the parent
+        q.put(repr(e))
+
+
+BLOCKS_RCCL = 32
+
+
+@pytest.mark.timeout(240)
+def test_rccl_world1_partial_path():
+    """the RCCL leg of dist.py (all-gathers of the partial and of the verdicts
+    through cuda:0 tensors) gives bgv_verify's verdicts, faulted and clean"""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_rank, args=(_free_port(), q))
+    p.start()
+    try:
+        res = q.get(timeout=200)
+    finally:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert isinstance(res, dict), res
+    expect = res["expect"]
+    assert res["shard"] == list(range(BLOCKS_RCCL))
+    valid, full, jr = res["faulted"]
+    assert (not valid) and full == expect and jr == expect
+    assert any(e != 1 for e in expect)
+    valid, full, jr = res["clean"]
+    assert valid and full == [1] * BLOCKS_RCCL and jr == full
