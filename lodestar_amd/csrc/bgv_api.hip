@@ -169,7 +169,7 @@ void bgv_cfg_default(bgv_cfg* cfg) {
   cfg->struct_size = sizeof *cfg;
   cfg->split = cfg->miller = cfg->msm = cfg->prefold = cfg->lines = cfg->defer_pct = cfg->timing = cfg->clear_lanes = -1;
   cfg->miller_kv = -1;
-  cfg->job_lanes = cfg->pairs = 0;
+  cfg->job_lanes = cfg->pairs = cfg->cu_split = 0;
 }
 
 int bgv_open(int device, bgv_ctx** out) { return bgv_open_cfg(device, nullptr, out); }
@@ -197,6 +197,7 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
     if (!tri_ok(k.prefold)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.prefold %d", k.prefold);
     if (!tri_ok(k.lines)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.lines %d", k.lines);
     if (!tri_ok(k.timing)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.timing %d", k.timing);
+    if (k.cu_split < -64 || k.cu_split > 64) return fail(BGV_E_INVALID_ARG, "bgv_cfg.cu_split %d (|N| <= 64 CUs)", k.cu_split);
     // two pairs per item exist only in the one-lane loop
     if (k.pairs == 2 && k.miller != -1 && k.miller != 1)
       return fail(BGV_E_INVALID_ARG, "bgv_cfg.pairs 2 needs the one-lane Miller loop (miller %d)", k.miller);
@@ -213,10 +214,28 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
   // lowest (it only feeds the signature tree and the 1 pair per job)
   int prio_lo = 0, prio_hi = 0;
   HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-  HIPCHK(hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, prio_lo));
-  HIPCHK(hipStreamCreateWithPriority(&c->st_hash, hipStreamNonBlocking, prio_hi));
-  HIPCHK(hipStreamCreateWithPriority(&c->st_pk, hipStreamNonBlocking, prio_hi));
-  HIPCHK(hipStreamCreateWithPriority(&c->st_chk, hipStreamNonBlocking, prio_lo));
+  if (k.cu_split == 0) {
+    HIPCHK(hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, prio_lo));
+    HIPCHK(hipStreamCreateWithPriority(&c->st_hash, hipStreamNonBlocking, prio_hi));
+    HIPCHK(hipStreamCreateWithPriority(&c->st_pk, hipStreamNonBlocking, prio_hi));
+    HIPCHK(hipStreamCreateWithPriority(&c->st_chk, hipStreamNonBlocking, prio_lo));
+  } else {
+    // CU partition between a priority context (the |N| highest CU ids) and the
+    // bulk contexts (the rest): a single set's few waves then never queue
+    // behind a resident bulk batch (k_hash alone holds two waves on every SIMD
+    // for ~16 ms at C4).  Streams with a CU mask take no priority.
+    int n_cu = 0;
+    HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
+    const int reserve = k.cu_split > 0 ? k.cu_split : -k.cu_split;
+    if (n_cu <= reserve) return fail(BGV_E_INVALID_ARG, "bgv_cfg.cu_split %d with %d CUs", k.cu_split, n_cu);
+    std::vector<uint32_t> mask((size_t)(n_cu + 31) / 32, 0u);
+    for (int cu = 0; cu < n_cu; cu++) {
+      const bool reserved = cu >= n_cu - reserve;
+      if (reserved == (k.cu_split > 0)) mask[cu / 32] |= 1u << (cu % 32);
+    }
+    hipStream_t* sts[4] = {&c->st, &c->st_hash, &c->st_pk, &c->st_chk};
+    for (hipStream_t* p : sts) HIPCHK(hipExtStreamCreateWithCUMask(p, (uint32_t)mask.size(), mask.data()));
+  }
   for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
   for (auto& e : c->ev_end) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipEventCreate(&c->ev_fork));

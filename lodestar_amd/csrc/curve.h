@@ -222,7 +222,11 @@ template <class F> BGV_NI void jac_mul_u64_w4(jac_t<F>& r, const jac_t<F>& p, ui
 // the addition as a call (one copy per unit): the x-chain and the cofactor
 // map below keep only their doubling inlined, so its temporaries stay in
 // registers instead of sharing a frame with the addition's
+#if defined(__HIPCC__) && BGV_ADD_CALL_INLINE
+template <class F> BGV_HD void jac_add_call(jac_t<F>& r, const jac_t<F>& p, const jac_t<F>& q) { jac_add(r, p, q); }
+#else
 template <class F> BGV_NI void jac_add_call(jac_t<F>& r, const jac_t<F>& p, const jac_t<F>& q) { jac_add(r, p, q); }
+#endif
 
 // [|x|]P for the BLS parameter: |x| = 0xd201000000010000 has its bits 63,
 // 62, 60, 57, 48 and 16 set, so after the top bit the double-and-add is runs

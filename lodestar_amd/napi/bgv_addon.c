@@ -5,13 +5,15 @@
  *   abiVersion() -> number                      bgv_abi_version
  *   buildId() -> string                         bgv_build_id
  *   codeName(code) -> "BLST_..."                 bgv_set_code_name
- *   open(device) -> ctx (external)               bgv_open      (multithread/index.ts:120)
+ *   open(device, cuSplit = 0) -> ctx (external)  bgv_open_cfg  (multithread/index.ts:120); cuSplit N > 0:
+ *                                                a priority context on N reserved CUs (verifyOnMainThread),
+ *                                                N < 0: a bulk context that leaves them free (bgv_cfg.cu_split)
  *   close(ctx)                                   bgv_close     (multithread/index.ts:193-214)
  *   pubkeysSet(ctx, first, Uint8Array, format)   bgv_pubkeys_set (pubkeyCache.ts:56-77)
  *   pubkeysCount(ctx) -> number
  *   pubkeysValidate(ctx, Uint8Array) -> Int32Array   bgv_pubkeys_validate (processDeposit.ts:57-66)
  *   verify(ctx, batch) -> Promise<result>        bgv_verify on the libuv pool (worker.ts:30-106)
- *   verifySync(ctx, batch) -> result             verifyOnMainThread / BlsSingleThreadVerifier
+ *   verifySync(ctx, batch) -> result             BlsSingleThreadVerifier (blocks the calling thread)
  *   partial(ctx, batch) -> Promise<result + {miller: Uint8Array(576), ok}>
  *                                                bgv_partial: one shard of a multi-GPU batch
  *   combineFinal(ctx, Uint8Array(576 n)) -> Promise<boolean>
@@ -135,13 +137,17 @@ static napi_value CodeName(napi_env env, napi_callback_info info) {
 }
 
 static napi_value Open(napi_env env, napi_callback_info info) {
-  size_t argc = 1;
-  napi_value a[1];
+  size_t argc = 2;
+  napi_value a[2];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, a, NULL, NULL));
-  int32_t dev = 0;
+  int32_t dev = 0, cu_split = 0;
   if (argc >= 1) NAPI_CALL(env, napi_get_value_int32(env, a[0], &dev));
+  if (argc >= 2) NAPI_CALL(env, napi_get_value_int32(env, a[1], &cu_split));
+  bgv_cfg cfg;
+  bgv_cfg_default(&cfg);
+  cfg.cu_split = cu_split;
   bgv_ctx* ctx = NULL;
-  const int st = bgv_open(dev, &ctx);
+  const int st = bgv_open_cfg(dev, &cfg, &ctx);
   if (st != BGV_OK) return throw_bgv(env, st);
   addon_ctx* c = (addon_ctx*)calloc(1, sizeof *c);
   c->ctx = ctx;

@@ -77,6 +77,8 @@ const MAX_BUFFERED_SIGS = 32; // multithread/index.ts:48
 const MAX_BUFFER_WAIT_MS = 100; // multithread/index.ts:57
 const MAX_JOBS_CAN_ACCEPT_WORK = 512; // multithread/index.ts:62
 const MAX_SETS_PER_DEVICE_BATCH = 1 << 17;
+const now = () => Number(process.hrtime.bigint()) / 1e6;
+const PRIORITY_CUS = 8; // CUs of the first device kept for verifyOnMainThread (bgv_cfg.cu_split)
 // a device batch of at least this many sets (and >= 2 jobs) is split by job
 // over the idle devices (partial Miller products, ONE combined final
 // exponentiation); smaller batches run whole on one device while the other
@@ -125,31 +127,40 @@ function aggregatedPubkeysCount(sets) {
   return n;
 }
 
-// jobs (arrays of sets) -> the SoA batch of include/bgv.h bgv_batch
+// jobs (arrays of sets) -> the SoA batch of include/bgv.h bgv_batch.  Two
+// passes (count, then fill typed arrays): a 2^17-set batch allocates its
+// arrays once instead of growing JS arrays of up to ~17M indices, which kept
+// the main thread in the garbage collector
 function encodeJobs(jobs) {
-  let n = 0;
-  for (const j of jobs) n += j.length;
+  let n = 0, nIdx = 0, nRaw = 0;
+  for (const j of jobs) {
+    n += j.length;
+    for (const s of j) {
+      const pks = s.type === "single" ? [s.pubkey] : s.pubkeys;
+      if (!pks || pks.length === 0) throw Error("EMPTY_AGGREGATE_ARRAY"); // PublicKey.aggregate, utils.ts:11
+      nIdx += pks.length;
+      for (const pk of pks) if (pk.raw) nRaw++;
+    }
+  }
   const jobOffsets = new Uint32Array(jobs.length + 1);
   const pkOffsets = new Uint32Array(n + 1);
-  const idx = [];
-  const raw = [];
+  const pkIndices = new Uint32Array(Math.max(nIdx, 1));
+  const rawPks = new Uint8Array(Math.max(nRaw, 1) * 96);
   const msgs = new Uint8Array(Math.max(n, 1) * 32);
   const sigs = new Uint8Array(Math.max(n, 1) * 192);
   const sigLen = new Uint32Array(Math.max(n, 1));
-  let i = 0;
+  let i = 0, x = 0, r = 0;
   jobs.forEach((job, k) => {
     for (const s of job) {
-      const pks = s.type === "single" ? [s.pubkey] : s.pubkeys;
-      if (!pks || pks.length === 0) throw Error("EMPTY_AGGREGATE_ARRAY"); // PublicKey.aggregate, utils.ts:11
-      for (const pk of pks) {
-        if (pk.raw) {
-          idx.push((RAW_BIT | raw.length) >>> 0);
-          raw.push(pk.raw);
-        } else {
-          idx.push(pk.index >>> 0);
+      if (s.type === "single") {
+        const pk = s.pubkey;
+        if (pk.raw) { pkIndices[x++] = (RAW_BIT | r) >>> 0; rawPks.set(pk.raw, 96 * r++); } else pkIndices[x++] = pk.index >>> 0;
+      } else {
+        for (const pk of s.pubkeys) {
+          if (pk.raw) { pkIndices[x++] = (RAW_BIT | r) >>> 0; rawPks.set(pk.raw, 96 * r++); } else pkIndices[x++] = pk.index >>> 0;
         }
       }
-      pkOffsets[i + 1] = idx.length;
+      pkOffsets[i + 1] = x;
       msgs.set(s.signingRoot, 32 * i);
       sigLen[i] = s.signature.length;
       if (s.signature.length === 96 || s.signature.length === 192) sigs.set(s.signature, 192 * i);
@@ -157,9 +168,7 @@ function encodeJobs(jobs) {
     }
     jobOffsets[k + 1] = i;
   });
-  const rawPks = new Uint8Array(Math.max(raw.length, 1) * 96);
-  raw.forEach((r, k) => rawPks.set(r, 96 * k));
-  return {jobOffsets, pkOffsets, pkIndices: Uint32Array.from(idx.length ? idx : [0]), msgs, sigs, sigLen, rawPks};
+  return {jobOffsets, pkOffsets, pkIndices, msgs, sigs, sigLen, rawPks};
 }
 
 // device work of a job in Montgomery Fp products (lodestar_amd/dist.py
@@ -228,7 +237,12 @@ class BlsGpuVerifier {
   // devices: HIP device ordinals, one context each, all owned by this process
   // (chain/chain.ts:199-202 constructs one verifier per node); every context
   // holds a replica of the pubkey table
-  constructor({device = 0, devices = null, maxSetsPerDeviceBatch = MAX_SETS_PER_DEVICE_BATCH, shardMinSets = SHARD_MIN_SETS} = {}) {
+  // priorityCus: CUs of the first device reserved for verifyOnMainThread
+  // (bgv_cfg.cu_split): a priority context runs there, the bulk context of
+  // that device leaves them free (~3% of its throughput for 8 of 256 CUs);
+  // 0 disables the reservation (the priority context then shares every CU)
+  constructor({device = 0, devices = null, maxSetsPerDeviceBatch = MAX_SETS_PER_DEVICE_BATCH, shardMinSets = SHARD_MIN_SETS,
+    priorityCus = PRIORITY_CUS} = {}) {
     const ids = devices && devices.length ? devices : [device];
     // every device batch holds a libuv pool thread (napi_async_work); the pool
     // size is read once, when the pool first starts, so the launcher must set
@@ -242,8 +256,12 @@ class BlsGpuVerifier {
       console.warn(`BlsGpuVerifier: ${ids.length} devices with ${was}: device batches may ` +
         "serialise and starve other pool work; start Node with UV_THREADPOOL_SIZE >= devices + 2");
     }
-    this.ctxs = ids.map((d) => addon.open(d));
+    this.ctxs = ids.map((d, k) => addon.open(d, k === 0 && priorityCus > 0 ? -priorityCus : 0));
     this.ctx = this.ctxs[0];
+    // verifyOnMainThread's own context (with its own table replica and mutex):
+    // it never waits for a bulk batch's context lock or, with priorityCus, its waves
+    this.prio = addon.open(ids[0], priorityCus > 0 ? priorityCus : 0);
+    this.prioBusy = 0;
     this.idle = ids.map(() => true);
     this.maxSetsPerDeviceBatch = maxSetsPerDeviceBatch;
     this.shardMinSets = shardMinSets;
@@ -263,7 +281,12 @@ class BlsGpuVerifier {
 
   // syncPubkeys / addPubkey (pubkeyCache.ts:56-77): 48-byte compressed keys, every replica
   syncPubkeys(firstIndex, pubkeys48) {
-    for (const c of this.ctxs) addon.pubkeysSet(c, firstIndex, pubkeys48, 0);
+    this.pubkeysSet(firstIndex, pubkeys48, 0);
+  }
+
+  // rows in either format (0: 48-byte compressed, 1: 96-byte uncompressed) into every replica
+  pubkeysSet(firstIndex, bytes, format) {
+    for (const c of this.ctxs.concat([this.prio])) addon.pubkeysSet(c, firstIndex, bytes, format);
   }
 
   // multithread/index.ts:143-149.  A queued job joins the next device batch,
@@ -279,21 +302,48 @@ class BlsGpuVerifier {
     if (this.closed) throw new QueueError();
     checkSets(sets);
     this.metrics.lodestar_bls_aggregated_pubkeys_total += aggregatedPubkeysCount(sets);
-    if (opts.verifyOnMainThread) {
-      // high priority, unbuffered: one synchronous device batch (an idle
-      // context if there is one; the context mutex serialises otherwise)
-      const k = Math.max(0, this.idle.indexOf(true));
-      const res = addon.verifySync(this.ctxs[k], encodeJobs([sets]));
-      this.recordWork([{sets}], res);
-      const o = jobOutcome(res.results[0]);
-      if (!o.ok) throw o.error;
-      return o.value;
-    }
+    if (opts.verifyOnMainThread) return this.verifyPriority(sets);
     const results = await Promise.all(
       chunkifyMaximizeChunkSize(sets, MAX_SIGNATURE_SETS_PER_JOB).map((chunk) => this.queueBlsWork(chunk, opts))
     );
     if (results.length === 0) throw Error("Empty results array");
     return results.every((r) => r === true);
+  }
+
+  // verifyOnMainThread (multithread/index.ts:155-167; chain/validation/block.ts:146
+  // for a gossip block's proposer signature): high priority and unbuffered, as
+  // the reference runs it at once on the main thread, but without blocking the
+  // event loop: one device batch on the priority context, on the libuv pool.
+  // It bypasses the buffer, the job queue and the bulk contexts' locks.
+  async verifyPriority(sets) {
+    this.prioBusy++;
+    try {
+      const t0 = now();
+      const batch = encodeJobs([sets]);
+      const t1 = now();
+      const pending = addon.verify(this.prio, batch);
+      this.lastPriorityIssue = {encodeMs: t1 - t0, queueMs: now() - t1};
+      const res = await pending;
+      this.recordWork([{sets}], res);
+      const o = jobOutcome(res.results[0]);
+      if (!o.ok) throw o.error;
+      return o.value;
+    } finally {
+      this.prioBusy--;
+    }
+  }
+
+  // BlsSingleThreadVerifier.verifySignatureSets (singleThread.ts:14-35):
+  // maybeBatch on the calling thread, for callers that want exactly that;
+  // the pool's verifyOnMainThread uses verifyPriority instead
+  verifySignatureSetsSync(sets) {
+    if (this.closed) throw new QueueError();
+    checkSets(sets);
+    const res = addon.verifySync(this.prio, encodeJobs([sets]));
+    this.recordWork([{sets}], res);
+    const o = jobOutcome(res.results[0]);
+    if (!o.ok) throw o.error;
+    return o.value;
   }
 
   // multithread/index.ts:255-292
@@ -486,11 +536,11 @@ class BlsGpuVerifier {
     for (const job of this.jobs) job.reject(new QueueError());
     this.jobs = [];
     this.queuedSets = 0;
-    for (const c of this.ctxs) addon.close(c); // each waits for its batch in flight (the context mutex)
+    for (const c of this.ctxs.concat([this.prio])) addon.close(c); // each waits for its batch in flight (the context mutex)
   }
 }
 
 module.exports = {
   addon, BlsGpuVerifier, QueueError, sourceHash, checkBuildId, chunkifyMaximizeChunkSize, encodeJobs, checkSets, shardJobs, jobWork,
-  MAX_BUFFERED_SIGS, MAX_BUFFER_WAIT_MS, MAX_JOBS_CAN_ACCEPT_WORK, SHARD_MIN_SETS,
+  MAX_BUFFERED_SIGS, MAX_BUFFER_WAIT_MS, MAX_JOBS_CAN_ACCEPT_WORK, SHARD_MIN_SETS, PRIORITY_CUS,
 };

@@ -25,7 +25,7 @@ BGV_E_TABLE_RANGE = -4
 BGV_E_EMPTY_SET = -5
 BGV_E_BAD_PUBKEY = -6
 BGV_E_STATE = -7
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 SET_CODE_NAMES = {
     0: "BLST_SUCCESS",
@@ -122,9 +122,9 @@ class BgvCfg(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32)] + [
         (k, ctypes.c_int32) for k in
         ("split", "miller", "job_lanes", "msm", "pairs", "prefold", "lines", "defer_pct", "timing", "clear_lanes",
-         "miller_kv")]
+         "miller_kv", "cu_split")]
     AUTO = {"split": -1, "miller": -1, "job_lanes": 0, "msm": -1, "pairs": 0, "prefold": -1, "lines": -1,
-            "defer_pct": -1, "timing": -1, "clear_lanes": -1, "miller_kv": -1}
+            "defer_pct": -1, "timing": -1, "clear_lanes": -1, "miller_kv": -1, "cu_split": 0}
 
     @classmethod
     def make(cls, **over) -> "BgvCfg":

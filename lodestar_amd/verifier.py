@@ -50,6 +50,7 @@ MAX_SIGNATURE_SETS_PER_JOB = 128  # multithread/index.ts:39
 MAX_BUFFERED_SIGS = 32            # multithread/index.ts:48
 MAX_BUFFER_WAIT_MS = 100          # multithread/index.ts:57
 MAX_JOBS_CAN_ACCEPT_WORK = 512    # multithread/index.ts:62
+PRIORITY_CUS = 8  # CUs of the first device kept for verifyOnMainThread (bgv_cfg.cu_split)
 MAX_SETS_PER_DEVICE_BATCH = 1 << 17
 # a device batch of at least this many sets (and >= 2 jobs) is split by job
 # over the idle devices: each returns a partial Miller product and ONE final
@@ -295,11 +296,19 @@ class BlsGpuVerifier:
     shard localises its own failing jobs (bgv_partial_finish)."""
 
     def __init__(self, devices=(0,), metrics: dict | None = None, scalar_seed: int | None = None,
-                 max_sets_per_device_batch: int = MAX_SETS_PER_DEVICE_BATCH, shard_min_sets: int = SHARD_MIN_SETS):
-        self.devices = [native.Device(d) for d in devices]
+                 max_sets_per_device_batch: int = MAX_SETS_PER_DEVICE_BATCH, shard_min_sets: int = SHARD_MIN_SETS,
+                 priority_cus: int = PRIORITY_CUS):
+        # priority_cus CUs of the first device are kept for verifyOnMainThread
+        # (bgv_cfg.cu_split): its own context runs there, the first bulk
+        # context leaves them free; 0 shares every CU
+        devices = list(devices)
+        self.devices = [native.Device(d, cu_split=-priority_cus) if k == 0 and priority_cus > 0 else native.Device(d)
+                        for k, d in enumerate(devices)]
+        self.prio = native.Device(devices[0], cu_split=priority_cus) if priority_cus > 0 else native.Device(devices[0])
+        self._prio_lock = threading.Lock()
         self._shard_min = shard_min_sets
         self._idle = [True] * len(self.devices)
-        self.table = PubkeyTable(self.devices)
+        self.table = PubkeyTable(self.devices + [self.prio])
         self.metrics = metrics if metrics is not None else _new_metrics()
         self._rng = np.random.default_rng(scalar_seed) if scalar_seed is not None else None
         self._max_batch = max_sets_per_device_batch
@@ -331,9 +340,10 @@ class BlsGpuVerifier:
         # device batch it shares with other callers
         check_sets(sets)
         if opts.verifyOnMainThread:
-            # unbuffered, high priority: one device batch right now
-            res = await asyncio.get_running_loop().run_in_executor(self._exec, self._run_device_batch, [sets], [0])
-            r = res[0]
+            # unbuffered, high priority (multithread/index.ts:155-167): one
+            # device batch on the priority context, off the event loop; it
+            # never waits for the bulk contexts' locks or waves
+            r = await asyncio.get_running_loop().run_in_executor(self._exec, self._run_priority, sets)
             if isinstance(r, Exception):
                 raise r
             return r
@@ -354,7 +364,7 @@ class BlsGpuVerifier:
         self._jobs.clear()
         self._buffered.clear()
         self._exec.shutdown(wait=True)
-        for d in self.devices:
+        for d in self.devices + [self.prio]:
             d.close()
 
     # -- synchronous helpers ------------------------------------------------
@@ -470,6 +480,18 @@ class BlsGpuVerifier:
         self.metrics["batch_retries"] += int(st.batch_retries)
         self.metrics["batch_sigs_success"] += int(st.batch_sigs_success)
         self.metrics["device_time_s"] += seconds
+
+    def _run_priority(self, sets: list[ISignatureSet]):
+        """verifyOnMainThread's device batch on the priority context"""
+        try:
+            arrays = encode_jobs([sets], self._scalars(len(sets)))
+            with self._prio_lock:
+                t0 = time.perf_counter()
+                jr, _ = self.prio.verify(arrays, want_set_codes=False)
+                self._record(self.prio.last_stats, time.perf_counter() - t0)
+        except Exception as e:  # noqa: BLE001 -- a device error rejects the call
+            return e
+        return self._verdict(int(jr[0]))
 
     def _run_device_batch(self, jobs: list[list[ISignatureSet]], devs: list[int] | None = None) -> list:
         """Verify a list of jobs on the devices `devs` (default: all); returns

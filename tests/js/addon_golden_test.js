@@ -64,8 +64,9 @@ async function main() {
   verifier.syncPubkeys(0, pk48);
   const extra = new Uint8Array(96 * v.extra_table.length);
   v.extra_table.forEach((p, k) => extra.set(hex(p), 96 * k));
-  addon.pubkeysSet(verifier.ctx, v.extra_table_base, extra, 1);
+  verifier.pubkeysSet(v.extra_table_base, extra, 1);
   assert.strictEqual(addon.pubkeysCount(verifier.ctx), interop.length + v.extra_table.length);
+  assert.strictEqual(addon.pubkeysCount(verifier.prio), interop.length + v.extra_table.length);
   assert.deepStrictEqual(Array.from(addon.pubkeysValidate(verifier.ctx, pk48.slice(0, 48 * 4))), [0, 0, 0, 0]);
   // a gap in the table and an undecodable key are refused
   assert.throws(() => addon.pubkeysSet(verifier.ctx, 5000, pk48.slice(0, 48), 0), /bgv error -4/);
@@ -93,6 +94,7 @@ async function main() {
   assert.strictEqual(await verifier.verifySignatureSets(sets), true);
   assert.strictEqual(await verifier.verifySignatureSets(sets, {batchable: true}), true);
   assert.strictEqual(await verifier.verifySignatureSets(sets, {verifyOnMainThread: true}), true);
+  assert.strictEqual(verifier.verifySignatureSetsSync(sets), true);  // BlsSingleThreadVerifier semantics
   const wrongMsg = sets.map((s, k) => (k === 1 ? {...s, signingRoot: hex(v.jobs[0].sets[0].msg).map((b) => b ^ 1)} : s));
   assert.strictEqual(await verifier.verifySignatureSets(wrongMsg), false);
   await assert.rejects(verifier.verifySignatureSets([{...sets[0], signature: new Uint8Array(32)}]), /BLST_INVALID_SIZE/);
@@ -189,7 +191,7 @@ async function main() {
   // combined final exponentiation; a failing shard is localised per job
   const multi = new BlsGpuVerifier({devices: [0, 0], shardMinSets: 1});
   multi.syncPubkeys(0, pk48);
-  multi.ctxs.forEach((c) => addon.pubkeysSet(c, v.extra_table_base, extra, 1));
+  multi.pubkeysSet(v.extra_table_base, extra, 1);
   const jobSets = v.jobs.map((j) => j.sets);
   const mres = await multi.verifySharded(goldenJobSets(v), [0, 1]);
   assert.strictEqual(mres.shards, 2);

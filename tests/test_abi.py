@@ -71,7 +71,7 @@ def test_struct_layout_matches_ctypes(tmp_path):
 
 def test_metadata_and_no_silent_fallback(lib):
     from lodestar_amd import native
-    assert lib.bgv_abi_version() == native.ABI_VERSION == 3
+    assert lib.bgv_abi_version() == native.ABI_VERSION == 4
     assert lib.bgv_set_code_name(8) == b"BLST_INVALID_SIZE"
     assert lib.bgv_set_code_name(3) == b"BLST_POINT_NOT_IN_GROUP"
     assert lib.bgv_stage_name(6) == b"miller_loop"
