@@ -219,9 +219,15 @@ template <class F> BGV_NI void jac_mul_u64_w4(jac_t<F>& r, const jac_t<F>& p, ui
   r = acc;
 }
 
-// the addition as a call (one copy per unit): the x-chain and the cofactor
-// map below keep only their doubling inlined, so its temporaries stay in
-// registers instead of sharing a frame with the addition's
+// the addition in the x-chain and the cofactor map.  As a call (one copy per
+// unit, BGV_ADD_CALL_INLINE=0) its temporaries do not share a frame with the
+// doubling's, but every call saves and restores the callee-saved VGPRs
+// through scratch; inlined, k_hash's frame grows (5,168 -> 6,224 B) and C4
+// still runs 0.25 ms faster (profiles/r05f_add_call_inline_ab.txt: 37.57
+// against 37.32 ms, A/B over three alternating pairs on one box)
+#ifndef BGV_ADD_CALL_INLINE
+#define BGV_ADD_CALL_INLINE 1
+#endif
 #if defined(__HIPCC__) && BGV_ADD_CALL_INLINE
 template <class F> BGV_HD void jac_add_call(jac_t<F>& r, const jac_t<F>& p, const jac_t<F>& q) { jac_add(r, p, q); }
 #else
