@@ -173,9 +173,9 @@ typedef struct bgv_cfg {
   int32_t clear_lanes;  /* -1 auto; 1 / 3 / 9 lanes per point of the latency mode's cofactor clearing */
   int32_t miller_kv;    /* -1 auto; 0 off; 2 / 3 / 6 / 9: the two-pair Miller loop in Karatsuba views on 6 / 9 / 18 / 27 lanes per two pairs */
   int32_t cu_split;     /* 0: every CU of the device (default).  N > 0: a PRIORITY context whose streams run only
-                           on N reserved CUs (the highest CU ids), for verifyOnMainThread single sets
-                           (multithread/index.ts:155-167) that must not wait for a bulk batch's waves;
-                           N < 0: a bulk context whose streams leave those |N| CUs free (ABI 4) */
+                           on N reserved CUs (the highest CU ids: with N = 8k, k CUs of every XCC), for
+                           verifyOnMainThread single sets (multithread/index.ts:155-167) that must not wait for a
+                           bulk batch's waves; N < 0: a bulk context whose streams leave those |N| CUs free (ABI 4) */
 } bgv_cfg;
 /* every field "auto" */
 void bgv_cfg_default(bgv_cfg* cfg);

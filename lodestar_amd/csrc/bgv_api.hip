@@ -223,7 +223,13 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
     // CU partition between a priority context (the |N| highest CU ids) and the
     // bulk contexts (the rest): a single set's few waves then never queue
     // behind a resident bulk batch (k_hash alone holds two waves on every SIMD
-    // for ~16 ms at C4).  Streams with a CU mask take no priority.
+    // for ~16 ms at C4).  Streams with a CU mask take no priority.  Mask bit i
+    // is CU i / 8 of XCC i % 8, in shader engine (i / 8) % 4
+    // (tools/cu_mask_probe.hip), and an XCC left without any bit runs on all of
+    // its CUs, so the highest 8k ids take k CUs from every XCC (32: one per
+    // SE).  Workgroups go round-robin over the SEs, so the bulk side runs at
+    // the pace of an SE that lost a CU: C4 +13% for 8, 16 or 32 reserved CUs
+    // alike (profiles/r05h_cu_split.txt), and the priority side gets 32.
     int n_cu = 0;
     HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
     const int reserve = k.cu_split > 0 ? k.cu_split : -k.cu_split;

@@ -78,7 +78,10 @@ const MAX_BUFFER_WAIT_MS = 100; // multithread/index.ts:57
 const MAX_JOBS_CAN_ACCEPT_WORK = 512; // multithread/index.ts:62
 const MAX_SETS_PER_DEVICE_BATCH = 1 << 17;
 const now = () => Number(process.hrtime.bigint()) / 1e6;
-const PRIORITY_CUS = 8; // CUs of the first device kept for verifyOnMainThread (bgv_cfg.cu_split)
+// CUs of the first device kept for verifyOnMainThread (bgv_cfg.cu_split): the top 32 ids are one CU of every
+// shader engine, and any reservation costs that device's bulk context ~13% (DESIGN.md §3), so the priority side
+// takes 32 rather than 8
+const PRIORITY_CUS = 32;
 // a device batch of at least this many sets (and >= 2 jobs) is split by job
 // over the idle devices (partial Miller products, ONE combined final
 // exponentiation); smaller batches run whole on one device while the other

@@ -50,7 +50,7 @@ MAX_SIGNATURE_SETS_PER_JOB = 128  # multithread/index.ts:39
 MAX_BUFFERED_SIGS = 32            # multithread/index.ts:48
 MAX_BUFFER_WAIT_MS = 100          # multithread/index.ts:57
 MAX_JOBS_CAN_ACCEPT_WORK = 512    # multithread/index.ts:62
-PRIORITY_CUS = 8  # CUs of the first device kept for verifyOnMainThread (bgv_cfg.cu_split)
+PRIORITY_CUS = 32  # CUs of the first device kept for verifyOnMainThread (bgv_cfg.cu_split; one per SE)
 MAX_SETS_PER_DEVICE_BATCH = 1 << 17
 # a device batch of at least this many sets (and >= 2 jobs) is split by job
 # over the idle devices: each returns a partial Miller product and ONE final

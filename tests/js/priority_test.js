@@ -10,7 +10,7 @@ const assert = require("assert");
 const fs = require("fs");
 const path = require("path");
 
-const {addon, BlsGpuVerifier, encodeJobs} = require(path.join(__dirname, "..", "..", "lodestar_amd", "napi"));
+const {addon, BlsGpuVerifier, encodeJobs, PRIORITY_CUS} = require(path.join(__dirname, "..", "..", "lodestar_amd", "napi"));
 const dir = process.argv[2];
 const rd = (name) => new Uint8Array(fs.readFileSync(path.join(dir, name)));
 const u32 = (name) => { const b = fs.readFileSync(path.join(dir, name)); return new Uint32Array(b.buffer, b.byteOffset, b.length / 4); };
@@ -31,11 +31,13 @@ async function main() {
 
   const verifier = new BlsGpuVerifier({device: 0});
   verifier.pubkeysSet(0, table, 1);
-  // warm both contexts (first-call allocations are not what is measured)
-  assert.strictEqual(await verifier.verifySignatureSets(bulkSets.slice(0, 256)), true);
+  // warm both contexts (first-call allocations are not what is measured) and
+  // the JIT: encodeJobs sees a bulk-sized input before the window, so the
+  // priority call inside it does not pay a deoptimisation for the new shapes
+  assert.strictEqual(await verifier.verifySignatureSets(bulkSets.slice(0, 8192)), true);
+  assert.strictEqual(await verifier.verifySignatureSets(single, {verifyOnMainThread: true}), true);
   assert.strictEqual(await verifier.verifySignatureSets(single, {verifyOnMainThread: true}), true);
 
-  if (global.gc) global.gc();
   const t0 = process.hrtime.bigint();
   const ms = () => Number(process.hrtime.bigint() - t0) / 1e6;
   // the synchronous part of a priority call with the device idle, piece by piece
@@ -48,27 +50,29 @@ async function main() {
     const d = ms();
     await p;
     const e = ms();
-    await verifier.verifySignatureSets(single, {verifyOnMainThread: true});
     idleIssue.encode = +(c - a).toFixed(3);
     idleIssue.addon_verify = +(d - c).toFixed(3);
     idleIssue.device = +(e - d).toFixed(3);
   }
+  // collect the set-up's garbage before the bulk call, not inside the window
+  if (global.gc) global.gc();
+  for (let k = 0; k < 4; k++) await new Promise((r) => setImmediate(r));
   let bulkDone = null, prioDone = null, prioStart = null;
+  const bulkStart = ms();
   const bulk = verifier.verifySignatureSets(bulkSets).then((v) => { bulkDone = ms(); return v; });
   // wait (event loop free) until the bulk device batch is in flight
   while (verifier.busy === 0) await new Promise((r) => setImmediate(r));
   const inflight = ms();
-  // collect the bulk encoding's garbage now, so a GC pause it would cause
-  // later does not land in the window
-  if (global.gc) global.gc();
-  // let V8 finish the collection's lazy sweeping on a few allocations before the window opens
-  for (let k = 0; k < 4; k++) {
-    const junk = new Array(4096).fill(k);
-    await new Promise((r) => setImmediate(r, junk));
-  }
-  const gcDone = ms();
+  // the bulk call's encoding leaves young garbage and new type feedback in
+  // verifySignatureSets / checkSets / encodeJobs: a minor collection and one
+  // priority call (awaited) take the one-time scavenge and re-optimisation
+  // outside the window, as in a node whose priority calls recur every slot
+  if (global.gc) global.gc({type: "minor"});
+  for (let k = 0; k < 4; k++) await new Promise((r) => setImmediate(r));
+  assert.strictEqual(await verifier.verifySignatureSets(single, {verifyOnMainThread: true}), true, "warm priority verdict");
+  const warmDone = ms();
   // the window: from the priority call until the bulk batch's device work
-  // completes (its result callback and the resolution of its 392 jobs are the
+  // completes (its result callback and the resolution of its jobs are the
   // pool's own bookkeeping on the main thread, as in the reference)
   let maxGap = 0, last = ms(), probes = 0, resultsAt = null;
   const record = verifier.recordWork.bind(verifier);
@@ -88,10 +92,6 @@ async function main() {
     };
     setImmediate(tick);
   });
-  // a first priority call absorbs the JIT's reaction to the bulk call's shapes
-  // (encodeJobs just ran on ~800 jobs); the window opens after it, with the
-  // measured call
-  const warm = verifier.verifySignatureSets(single, {verifyOnMainThread: true});
   await new Promise((r) => setImmediate(r));
   last = ms();
   const probing = probe();
@@ -99,12 +99,11 @@ async function main() {
   const prio = verifier.verifySignatureSets(single, {verifyOnMainThread: true}).then((v) => { prioDone = ms(); return v; });
   const prioIssued = ms();
   const issueParts = verifier.lastPriorityIssue;
-  const [bv, pv, wv] = await Promise.all([bulk, prio, warm]);
-  assert.strictEqual(wv, true, "first priority verdict");
+  const [bv, pv] = await Promise.all([bulk, prio]);
   await probing;
-  console.log(JSON.stringify({n_bulk: bulkSets.length, bulk_in_flight_ms: inflight, gc_ms: gcDone - inflight, prio_start_ms: prioStart, prio_issue_ms: prioIssued - prioStart, issue_parts: issueParts, idle_issue: idleIssue,
+  console.log(JSON.stringify({n_bulk: bulkSets.length, bulk_start_ms: bulkStart, bulk_in_flight_ms: inflight, warm_done_ms: warmDone, prio_start_ms: prioStart, prio_issue_ms: prioIssued - prioStart, issue_parts: issueParts, idle_issue: idleIssue,
     prio_done_ms: prioDone, bulk_done_ms: bulkDone, prio_latency_ms: prioDone - prioStart, max_event_loop_gap_ms: maxGap,
-    bulk_results_at_ms: resultsAt, probes, gaps_over_1ms: gaps, prio_cus: verifier.prio ? 8 : 0}));
+    bulk_results_at_ms: resultsAt, probes, gaps_over_1ms: gaps, prio_cus: PRIORITY_CUS}));
   assert.strictEqual(bv, true, "bulk verdict");
   assert.strictEqual(pv, true, "priority verdict");
   assert.ok(prioDone < bulkDone, `priority call resolved after the bulk batch (${prioDone} >= ${bulkDone} ms)`);

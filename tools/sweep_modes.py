@@ -19,6 +19,12 @@ sys.path.insert(0, ROOT)
 
 MODES = {  # bgv_cfg overrides (include/bgv.h)
     "default": {},
+    "bulk_cu8": {"cu_split": -8},  # the Node pool's bulk context beside a priority context (r05)
+    "prio_cu8": {"cu_split": 8},  # the priority context itself on 8 reserved CUs
+    "bulk_cu32": {"cu_split": -32},
+    "prio_cu32": {"cu_split": 32},
+    "bulk_cu16": {"cu_split": -16},
+    "prio_cu16": {"cu_split": 16},
     "split0": {"split": 0},
     "split0_serial": {"split": 0, "miller": 1},
     "split0_serial_msm": {"split": 0, "miller": 1, "msm": 1},
