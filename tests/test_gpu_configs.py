@@ -112,6 +112,11 @@ def test_c2_gossip_batch(big):
     a = _sign(big, a)
     jr, sc = big.verify(a)
     assert jr.tolist() == [1] and (sc == 0).all()
+    _cref_block_check(big, a, [0], [1])
+    # the bad call's job (set 5 signed over set 6's message) fails in the C restatement too
+    wrong = dict(a, msgs=a["msgs"].copy())
+    wrong["msgs"][5] = a["msgs"][6]
+    _cref_block_check(big, wrong, [0], [0])
     sets = G.sets_from_arrays(a)[0]
 
     async def run(pool):
@@ -139,7 +144,7 @@ def test_c3_blocks_first_invalid(coalesce, att_k):
     try:
         d = pool.devices[0]
         d.gen_keys(0, N_TABLE, SEED)
-        blocks = []
+        blocks, arrays = [], []
         for b in range(3):
             a = bench.build_segment([b], seed=SEED + 2000, att_per_block=128, att_k=att_k)
             assert a["n_sets"] == 131 and int(a["pk_offsets"][-1]) == 128 * att_k + 512 + 2
@@ -149,12 +154,15 @@ def test_c3_blocks_first_invalid(coalesce, att_k):
             s = _sign(d, dict(a, msgs=sign_msgs))
             s["msgs"] = a["msgs"]
             blocks.append(G.sets_from_arrays(s)[0])
+            arrays.append(s)
 
         async def run(bl):
             return await V.verify_blocks_signatures(pool, bl, coalesce=coalesce)
 
         assert asyncio.run(run(blocks)) == {"allValid": False, "index": 1}
         assert asyncio.run(run([blocks[0], blocks[2]])) == {"allValid": True}
+        for b, s in enumerate(arrays):  # each block re-verified by the C restatement
+            _cref_block_check(d, s, [0], [0 if b == 1 else 1])
     finally:
         asyncio.run(pool.close())
 
