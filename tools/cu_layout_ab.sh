@@ -1,6 +1,8 @@
 #!/bin/bash
 # Bulk (cu_split -8) and priority (cu_split 8) contexts under the reserved-CU
-# layouts of variant libraries (BGV_CU_RESERVE_LAYOUT), against the full chip.
+# layouts of variant libraries, against the full chip (r05: the BGV_CU_RESERVE_LAYOUT
+# knob these were built with is gone; tools/cu_mask_probe.hip showed why its
+# spread layouts were wrong: they put every reserved CU on one XCC).
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
