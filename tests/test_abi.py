@@ -111,7 +111,8 @@ def test_cfg_defaults_and_validation(lib):
     h = ctypes.c_void_p()
     # invalid overrides are refused before any device call (no GPU needed)
     for bad in ({"miller": 7}, {"job_lanes": 5}, {"pairs": 3}, {"defer_pct": 101}, {"split": 2}, {"prefold": -2},
-                {"lines": 2}, {"timing": 5}, {"miller": 4, "pairs": 2}, {"miller": 36, "pairs": 2}):
+                {"lines": 2}, {"timing": 5}, {"miller": 4, "pairs": 2}, {"miller": 36, "pairs": 2},
+                {"cu_split": 65}, {"cu_split": -65}, {"clear_lanes": 2}, {"miller_kv": 4}):
         st = lib.bgv_open_cfg(0, ctypes.byref(native.BgvCfg.make(**bad)), ctypes.byref(h))
         assert st == native.BGV_E_INVALID_ARG, bad
     c2 = native.BgvCfg.make()

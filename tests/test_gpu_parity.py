@@ -51,6 +51,24 @@ def test_golden_each_job_alone(dev, job):
     assert sc.tolist() == codes
 
 
+@pytest.mark.parametrize("cu_split", [32, -32, 8])
+def test_golden_batch_on_partitioned_cus(cu_split):
+    """the priority context (cu_split > 0: streams on reserved CUs) and the
+    bulk context beside it (< 0) give the golden verdicts and set codes"""
+    from lodestar_amd import native
+    d = native.Device(0, cu_split=cu_split)
+    try:
+        G.load_golden_table(d)
+        arrays, expected, codes = G.golden_arrays()
+        jr, sc = d.verify(arrays)
+        assert jr.tolist() == expected
+        assert sc.tolist() == codes
+        valid, _, _ = G.golden_arrays([0, 1, 9])
+        assert d.verify(valid)[0].tolist() == [1, 1, 1]
+    finally:
+        d.close()
+
+
 def test_golden_valid_jobs_single_batch_check(dev):
     valid = [0, 1, 9, 11, 12, 13]
     arrays, expected, _ = G.golden_arrays(valid)
