@@ -241,7 +241,10 @@ void launch_miller_kv(hipStream_t st, const dev_batch& b, const dev_work& w) {
 
 // the unevaluated lines of every set's H(m) (pairing.h miller_lines), on the
 // hash stream right after k_hash: one lane per set
-__global__ void __launch_bounds__(64, 2) k_lines(dev_batch b, dev_work w) {
+#ifndef BGV_LINES_WAVES
+#define BGV_LINES_WAVES 2
+#endif
+__global__ void __launch_bounds__(64, BGV_LINES_WAVES) k_lines(dev_batch b, dev_work w) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= b.n_sets) return;
   miller_lines(w.lines, b.n_sets, i, w.h_aff[i]);
