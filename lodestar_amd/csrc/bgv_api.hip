@@ -634,11 +634,13 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   const int pct = !deferrable ? 0 : (k.defer_pct >= 0 ? k.defer_pct : (!d.split && d.pairs_per_item == 2 ? 75 : 100));
   d.defer_grp = pct > 0 ? 1u : 0u;
   d.defer_from = pct > 0 ? (uint32_t)(((uint64_t)n * (uint32_t)(100 - pct) / 100u) & ~63ull) : n;
-  // two-level per-job fold (bgv_tail.hip) when few jobs of >= 64 sets leave
-  // the chip idle: groups of ~sqrt(span) sets fold side by side, then the job
-  // folds the group values, 2 sqrt(span) sequential Fp12 products instead of span
+  // two-level per-job fold (bgv_tail.hip) for jobs of >= 64 sets: the fold
+  // runs after the Miller kernels with the chip otherwise idle, so groups of
+  // ~sqrt(span) sets fold side by side, then the job folds the group values,
+  // 2 sqrt(span) sequential Fp12 products instead of span (r05: also for many
+  // jobs; C4 product-tree stage 0.36 -> 0.33 ms, profiles/r05l_job_fold.txt)
   {
-    const bool few_big = d.n_jobs <= 256 && d.span_log2 >= 6 && d.span_log2 <= 8;
+    const bool few_big = d.span_log2 >= 6 && d.span_log2 <= 8;
     const bool on = k.prefold >= 0 ? (k.prefold && d.span_log2 >= 2 && d.span_log2 <= 8) : few_big;
     d.prefold_log2 = on ? (d.span_log2 + 1) / 2 : 0u;
   }

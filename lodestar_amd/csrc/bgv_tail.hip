@@ -57,10 +57,17 @@ __global__ void BGV_TREE_LB k_job_f(dev_batch b, dev_work w, uint32_t span) {
 // ------------------------------------------- cooperative folds (fp12_coop.h)
 #define COOP_LB __launch_bounds__(COOP_THREADS, 2)
 
+// With two pairs per Miller item the item's value sits at the even offsets of
+// the job and every odd entry is 1 (k_miller, k_miller_kv), so the folds step
+// over the items only: at C4 that halves the per-job chain (98 -> 49 Fp12
+// products).
+__device__ __forceinline__ static uint32_t fold_step(const dev_batch& b) { return b.pairs_per_item == 2 ? 2u : 1u; }
+
 // first level of the two-level fold (few large jobs, e.g. one 64-set gossip
-// batch): workgroup (g, j) folds the job's sets [beg + G g, beg + G g + G)
-// into f_set[beg + G g] (in place: all reads precede the one write, and the
-// groups are disjoint); k_job_fold then walks the job with stride G
+// batch, and the C4 segment's 98-set blocks): workgroup (g, j) folds the job's
+// values in [beg + G g, beg + G g + G) into f_set[beg + G g] (in place: all
+// reads precede the one write, and the groups are disjoint); k_job_fold then
+// walks the job with stride G
 __global__ void COOP_LB k_job_prefold(dev_batch b, dev_work w) {
   __shared__ cscratch s;
   __shared__ wfp12 acc, x;
@@ -70,7 +77,7 @@ __global__ void COOP_LB k_job_prefold(dev_batch b, dev_work w) {
   if (w.job_code[j] != C_OK || g0 + 1 >= end) return;  // uniform per workgroup
   const uint32_t g1 = min(end, g0 + G);
   c_load(&acc, w.f_set[g0]);
-  for (uint32_t i = g0 + 1; i < g1; i++) {
+  for (uint32_t i = g0 + fold_step(b); i < g1; i += fold_step(b)) {
     c_load(&x, w.f_set[i]);
     c_mul(&acc, &acc, &x, &s);
   }
@@ -177,7 +184,7 @@ void launch_fp12_tail(hipStream_t st, int stage, const dev_batch& b, const dev_w
   if (stage == ST_F_TREE) {
     if (!b.n_jobs) return;
     if (span <= 256) {  // every job folds in one workgroup
-      uint32_t stride = 1;
+      uint32_t stride = b.pairs_per_item == 2 ? 2u : 1u;  // fold_step
       if (b.prefold_log2) {  // few large jobs: fold groups side by side first
         stride = 1u << b.prefold_log2;
         hipLaunchKernelGGL(k_job_prefold, dim3((span + stride - 1) / stride, b.n_jobs), ct, 0, st, b, w);

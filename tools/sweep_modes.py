@@ -21,6 +21,8 @@ MODES = {  # bgv_cfg overrides (include/bgv.h)
     "default": {},
     "bulk_cu8": {"cu_split": -8},  # the Node pool's bulk context beside a priority context (r05)
     "prio_cu8": {"cu_split": 8},  # the priority context itself on 8 reserved CUs
+    "prefold1": {"prefold": 1},
+    "prefold0": {"prefold": 0},
     "bulk_cu32": {"cu_split": -32},
     "prio_cu32": {"cu_split": 32},
     "bulk_cu16": {"cu_split": -16},
