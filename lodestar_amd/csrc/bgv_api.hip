@@ -789,7 +789,12 @@ static int run_stages(bgv_ctx* c, const dev_batch& d, const dev_work& w, int fro
   // latency batches fork the hash leg BEFORE the index set-up: hash_to_G2 reads
   // only the messages and heads the critical path (hash -> Miller -> fold ->
   // final exp); large batches keep the set-up alone on the GPU (its
-  // one-workgroup scan starves under the bulk kernels)
+  // one-workgroup scan starves under the bulk kernels).  At C4 the signature
+  // decode is dispatched first, on the set-up's own stream: dispatching the
+  // hash first ends it at ~12.5 instead of ~16.3 ms, but the signature chain
+  // (decode -> MSM buckets -> window sums -> job pairs, ~32 ms of the 37)
+  // then runs into the Miller phase, and the step lost 0.2-3.8 ms in every
+  // order tried (profiles/r05m_bulk_stage_order.txt)
   const bool early_hash = fork && d.split && from <= ST_HASH && to > ST_HASH;
   auto launch_one = [&](int s) -> int {
     hipStream_t st = c->st;
