@@ -22,6 +22,8 @@ MODES = {  # bgv_cfg overrides (include/bgv.h)
     "bulk_cu8": {"cu_split": -8},  # the Node pool's bulk context beside a priority context (r05)
     "prio_cu8": {"cu_split": 8},  # the priority context itself on 8 reserved CUs
     "prefold1": {"prefold": 1},
+    "msm4": {"msm": 4},
+    "msm4d100": {"msm": 4, "defer_pct": 100},
     "prefold0": {"prefold": 0},
     "bulk_cu32": {"cu_split": -32},
     "prio_cu32": {"cu_split": 32},
