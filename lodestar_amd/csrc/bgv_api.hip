@@ -665,6 +665,9 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
     d.miller_kv = k.miller_kv >= 0 ? (uint32_t)k.miller_kv : auto_kv;
     if (!d.split) d.miller_kv = 0;
     if (d.miller_kv) d.pairs_per_item = 2;
+    // the cooperative, four- and two-lane loops hold one pair per item (every
+    // set has its own Miller value, which the per-job fold relies on)
+    else if (d.miller_coop) d.pairs_per_item = 1;
   }
   // fixed-argument lines (pairing.h miller_lines): the G2 half of the one-lane
   // Miller loop moves to the hash stream, phase 1 (C4 40.4 -> 39.5 ms); with
