@@ -23,6 +23,9 @@ MODES = {  # bgv_cfg overrides (include/bgv.h)
     "prio_cu8": {"cu_split": 8},  # the priority context itself on 8 reserved CUs
     "prefold1": {"prefold": 1},
     "msm4": {"msm": 4},
+    "d100": {"defer_pct": 100},
+    "d90": {"defer_pct": 90},
+    "d60": {"defer_pct": 60},
     "msm4d100": {"msm": 4, "defer_pct": 100},
     "prefold0": {"prefold": 0},
     "bulk_cu32": {"cu_split": -32},
