@@ -49,20 +49,30 @@ def batch_job_work(arrays: dict) -> list[float]:
     return job_work(sets.tolist(), refs.tolist())
 
 
-def shard_jobs(job_weights, world: int) -> list[list[int]]:
+def shard_jobs(job_weights, world: int, caps=None) -> list[list[int]]:
     """Whole jobs to ranks, greedy by work (largest first, each to the least
     loaded rank), job order kept inside a shard.  A job is never split (its
     verdict is an AND of its sets).  job_weights: batch_job_work / job_work,
-    or set counts."""
+    or set counts.  caps: relative speed of each rank (default all 1); load is
+    compared as load / cap, so a device whose bulk context leaves CUs to a
+    priority context (RESERVED_CAP) gets a proportionally smaller shard."""
     shards: list[list[int]] = [[] for _ in range(world)]
     load = [0.0] * world
+    cap = [1.0] * world if caps is None else [float(c) for c in caps]
     w = [float(x) for x in job_weights]
     floor = min((x for x in w if x > 0), default=1.0)  # an empty job still costs a slot
     for j in sorted(range(len(w)), key=lambda j: (-w[j], j)):
-        r = load.index(min(load))
+        r = min(range(world), key=lambda k: (load[k] / cap[k], k))
         shards[r].append(j)
         load[r] += max(w[j], floor)
     return [sorted(s) for s in shards]
+
+
+# throughput of a device whose bulk context reserves CUs for a priority context
+# (bgv_cfg.cu_split < 0): workgroups go round-robin over the shader engines, so
+# the bulk context runs at the pace of an engine with 7 of its 8 CUs
+# (DESIGN.md §3 r05: C4 36.8 -> 41.7 ms)
+RESERVED_CAP = 7.0 / 8.0
 
 
 def shard_balance(job_weights, shards) -> float:

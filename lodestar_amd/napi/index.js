@@ -82,6 +82,7 @@ const now = () => Number(process.hrtime.bigint()) / 1e6;
 // shader engine, and any reservation costs that device's bulk context ~13% (DESIGN.md §3), so the priority side
 // takes 32 rather than 8
 const PRIORITY_CUS = 32;
+const RESERVED_CAP = 7 / 8; // dist.py RESERVED_CAP: bulk pace of a device with reserved CUs
 // a device batch of at least this many sets (and >= 2 jobs) is split by job
 // over the idle devices (partial Miller products, ONE combined final
 // exponentiation); smaller batches run whole on one device while the other
@@ -186,17 +187,19 @@ function jobWork(sets) {
 }
 
 // whole jobs to `world` shards, greedy by work (largest first, each to the
-// least loaded shard), job order kept inside a shard (dist.py shard_jobs)
-function shardJobs(weights, world) {
+// least loaded shard), job order kept inside a shard (dist.py shard_jobs);
+// caps: relative speed per shard (load compared as load / cap)
+function shardJobs(weights, world, caps = null) {
   const shards = Array.from({length: world}, () => []);
   const load = new Array(world).fill(0);
+  const cap = caps || new Array(world).fill(1);
   let floor = Infinity;
   for (const w of weights) if (w > 0 && w < floor) floor = w;
   if (floor === Infinity) floor = 1;
   const order = weights.map((s, j) => j).sort((a, b) => weights[b] - weights[a] || a - b);
   for (const j of order) {
     let r = 0;
-    for (let k = 1; k < world; k++) if (load[k] < load[r]) r = k;
+    for (let k = 1; k < world; k++) if (load[k] / cap[k] < load[r] / cap[r]) r = k;
     shards[r].push(j);
     load[r] += Math.max(weights[j], floor);
   }
@@ -242,8 +245,10 @@ class BlsGpuVerifier {
   // holds a replica of the pubkey table
   // priorityCus: CUs of the first device reserved for verifyOnMainThread
   // (bgv_cfg.cu_split): a priority context runs there, the bulk context of
-  // that device leaves them free (~3% of its throughput for 8 of 256 CUs);
-  // 0 disables the reservation (the priority context then shares every CU)
+  // that device leaves them free (~13% of its throughput whatever the count:
+  // the shader engines that lost a CU set the pace; sharded batches give that
+  // device a proportionally smaller shard); 0 disables the reservation (the
+  // priority context then shares every CU)
   constructor({device = 0, devices = null, maxSetsPerDeviceBatch = MAX_SETS_PER_DEVICE_BATCH, shardMinSets = SHARD_MIN_SETS,
     priorityCus = PRIORITY_CUS} = {}) {
     const ids = devices && devices.length ? devices : [device];
@@ -264,6 +269,7 @@ class BlsGpuVerifier {
     // verifyOnMainThread's own context (with its own table replica and mutex):
     // it never waits for a bulk batch's context lock or, with priorityCus, its waves
     this.prio = addon.open(ids[0], priorityCus > 0 ? priorityCus : 0);
+    this.prioReserved = priorityCus > 0;
     this.prioBusy = 0;
     this.idle = ids.map(() => true);
     this.maxSetsPerDeviceBatch = maxSetsPerDeviceBatch;
@@ -473,7 +479,10 @@ class BlsGpuVerifier {
   // does each shard localise its failing jobs (bgv_partial_finish, the
   // worker's per-job retry).  Returns the result shape of addon.verify.
   async verifySharded(jobSets, devs) {
-    const shards = shardJobs(jobSets.map(jobWork), devs.length);
+    // the first device's bulk context leaves CUs to the priority context and
+    // runs at RESERVED_CAP of the others' pace (dist.py)
+    const caps = devs.map((d) => (d === 0 && this.prioReserved ? RESERVED_CAP : 1));
+    const shards = shardJobs(jobSets.map(jobWork), devs.length, caps);
     const live = [];
     shards.forEach((ids, r) => ids.length && live.push({ctx: this.ctxs[devs[r]], ids}));
     if (live.length === 1) return addon.verify(live[0].ctx, encodeJobs(jobSets));
@@ -545,5 +554,5 @@ class BlsGpuVerifier {
 
 module.exports = {
   addon, BlsGpuVerifier, QueueError, sourceHash, checkBuildId, chunkifyMaximizeChunkSize, encodeJobs, checkSets, shardJobs, jobWork,
-  MAX_BUFFERED_SIGS, MAX_BUFFER_WAIT_MS, MAX_JOBS_CAN_ACCEPT_WORK, SHARD_MIN_SETS, PRIORITY_CUS,
+  MAX_BUFFERED_SIGS, MAX_BUFFER_WAIT_MS, MAX_JOBS_CAN_ACCEPT_WORK, SHARD_MIN_SETS, PRIORITY_CUS, RESERVED_CAP,
 };

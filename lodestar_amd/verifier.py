@@ -44,7 +44,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import native
-from .dist import job_work, shard_jobs
+from .dist import RESERVED_CAP, job_work, shard_jobs
 
 MAX_SIGNATURE_SETS_PER_JOB = 128  # multithread/index.ts:39
 MAX_BUFFERED_SIGS = 32            # multithread/index.ts:48
@@ -305,6 +305,7 @@ class BlsGpuVerifier:
         self.devices = [native.Device(d, cu_split=-priority_cus) if k == 0 and priority_cus > 0 else native.Device(d)
                         for k, d in enumerate(devices)]
         self.prio = native.Device(devices[0], cu_split=priority_cus) if priority_cus > 0 else native.Device(devices[0])
+        self.prio_reserved = priority_cus > 0  # device 0's bulk context runs at RESERVED_CAP (shard_jobs caps)
         self._prio_lock = threading.Lock()
         self._shard_min = shard_min_sets
         self._idle = [True] * len(self.devices)
@@ -506,7 +507,8 @@ class BlsGpuVerifier:
         devs = list(range(len(self.devices))) if devs is None else list(devs)
         if len(devs) > 1:
             refs = [sum(1 if s.type == SignatureSetType.single else len(s.pubkeys) for s in j) for j in jobs]
-            shards = shard_jobs(job_work([len(j) for j in jobs], refs), len(devs))
+            caps = [RESERVED_CAP if d == 0 and self.prio_reserved else 1.0 for d in devs]
+            shards = shard_jobs(job_work([len(j) for j in jobs], refs), len(devs), caps)
         else:
             shards = [list(range(len(jobs)))]
         live = [(devs[r], ids) for r, ids in enumerate(shards) if ids]

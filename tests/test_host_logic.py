@@ -128,6 +128,23 @@ def test_shard_jobs_balance_work_on_a_mixed_segment():
     assert a > b
 
 
+def test_shard_jobs_weights_a_reserved_device():
+    """a device whose bulk context leaves CUs to the priority context runs at
+    RESERVED_CAP: it gets a proportionally smaller shard, so the shards finish
+    together (load / cap within 5% max/mean)"""
+    from lodestar_amd.dist import RESERVED_CAP
+    jobs = mixed_segment_jobs()
+    work = job_work([s for s, _ in jobs], [k for _, k in jobs])
+    for world in (2, 4, 8):
+        caps = [RESERVED_CAP] + [1.0] * (world - 1)
+        shards = shard_jobs(work, world, caps)
+        assert sorted(j for s in shards for j in s) == list(range(len(jobs)))
+        t = [sum(work[j] for j in sh) / c for sh, c in zip(shards, caps)]
+        assert max(t) / (sum(t) / world) <= 1.05, world
+        assert sum(work[j] for j in shards[0]) < min(sum(work[j] for j in sh) for sh in shards[1:])
+    assert shard_jobs(work, 4, [1.0] * 4) == shard_jobs(work, 4)
+
+
 def test_batch_job_work_matches_job_work():
     jo = np.array([0, 2, 5, 5, 6], np.uint32)
     po = np.array([0, 1, 513, 641, 642, 643, 771], np.uint32)
@@ -147,8 +164,12 @@ def test_node_shard_jobs_is_the_python_assignment():
     for (s, k), js in zip(jobs, sets):
         js[0]["pubkeys"] = [0] * (k - (k // s) * (s - 1))
     script = ("const m = require(%r); const jobs = JSON.parse(require('fs').readFileSync(0, 'utf8'));"
-              "console.log(JSON.stringify([8, 4, 2].map((w) => m.shardJobs(jobs.map(m.jobWork), w))));") % os.path.join(
+              "const caps = (w) => [m.RESERVED_CAP].concat(new Array(w - 1).fill(1));"
+              "console.log(JSON.stringify([8, 4, 2].map((w) => m.shardJobs(jobs.map(m.jobWork), w))"
+              ".concat([8, 4, 2].map((w) => m.shardJobs(jobs.map(m.jobWork), w, caps(w))))));") % os.path.join(
                   ROOT, "lodestar_amd", "napi", "index.js")
     out = json.loads(subprocess.check_output(["node", "-e", script], input=json.dumps(sets).encode()))
     work = job_work([s for s, _ in jobs], [k for _, k in jobs])
-    assert out == [shard_jobs(work, w) for w in (8, 4, 2)]
+    from lodestar_amd.dist import RESERVED_CAP
+    assert out == [shard_jobs(work, w) for w in (8, 4, 2)] + [shard_jobs(work, w, [RESERVED_CAP] + [1.0] * (w - 1))
+                                                              for w in (8, 4, 2)]
