@@ -249,8 +249,12 @@ class BlsGpuVerifier {
   // the shader engines that lost a CU set the pace; sharded batches give that
   // device a proportionally smaller shard); 0 disables the reservation (the
   // priority context then shares every CU)
+  // blsVerifyAllMultiThread (chain/options.ts:14, multithread/index.ts:124): verifyOnMainThread
+  // calls join the pool's queue like any other; no CUs are then reserved
   constructor({device = 0, devices = null, maxSetsPerDeviceBatch = MAX_SETS_PER_DEVICE_BATCH, shardMinSets = SHARD_MIN_SETS,
-    priorityCus = PRIORITY_CUS} = {}) {
+    priorityCus = PRIORITY_CUS, blsVerifyAllMultiThread = false} = {}) {
+    if (blsVerifyAllMultiThread) priorityCus = 0;
+    this.blsVerifyAllMultiThread = blsVerifyAllMultiThread;
     const ids = devices && devices.length ? devices : [device];
     // every device batch holds a libuv pool thread (napi_async_work); the pool
     // size is read once, when the pool first starts, so the launcher must set
@@ -311,7 +315,7 @@ class BlsGpuVerifier {
     if (this.closed) throw new QueueError();
     checkSets(sets);
     this.metrics.lodestar_bls_aggregated_pubkeys_total += aggregatedPubkeysCount(sets);
-    if (opts.verifyOnMainThread) return this.verifyPriority(sets);
+    if (opts.verifyOnMainThread && !this.blsVerifyAllMultiThread) return this.verifyPriority(sets);
     const results = await Promise.all(
       chunkifyMaximizeChunkSize(sets, MAX_SIGNATURE_SETS_PER_JOB).map((chunk) => this.queueBlsWork(chunk, opts))
     );

@@ -297,10 +297,15 @@ class BlsGpuVerifier:
 
     def __init__(self, devices=(0,), metrics: dict | None = None, scalar_seed: int | None = None,
                  max_sets_per_device_batch: int = MAX_SETS_PER_DEVICE_BATCH, shard_min_sets: int = SHARD_MIN_SETS,
-                 priority_cus: int = PRIORITY_CUS):
+                 priority_cus: int = PRIORITY_CUS, bls_verify_all_multi_thread: bool = False):
         # priority_cus CUs of the first device are kept for verifyOnMainThread
         # (bgv_cfg.cu_split): its own context runs there, the first bulk
-        # context leaves them free; 0 shares every CU
+        # context leaves them free; 0 shares every CU.
+        # bls_verify_all_multi_thread (chain/options.ts:14, multithread/index.ts:124):
+        # verifyOnMainThread calls join the queue like any other, no CUs reserved
+        if bls_verify_all_multi_thread:
+            priority_cus = 0
+        self.bls_verify_all_multi_thread = bls_verify_all_multi_thread
         devices = list(devices)
         self.devices = [native.Device(d, cu_split=-priority_cus) if k == 0 and priority_cus > 0 else native.Device(d)
                         for k, d in enumerate(devices)]
@@ -340,7 +345,7 @@ class BlsGpuVerifier:
         # (getAggregatedPubkey, utils.ts:5-16), so a bad call cannot fail a
         # device batch it shares with other callers
         check_sets(sets)
-        if opts.verifyOnMainThread:
+        if opts.verifyOnMainThread and not self.bls_verify_all_multi_thread:
             # unbuffered, high priority (multithread/index.ts:155-167): one
             # device batch on the priority context, off the event loop; it
             # never waits for the bulk contexts' locks or waves

@@ -93,7 +93,9 @@ async function main() {
   }));
   assert.strictEqual(await verifier.verifySignatureSets(sets), true);
   assert.strictEqual(await verifier.verifySignatureSets(sets, {batchable: true}), true);
+  const groups0 = verifier.metrics.lodestar_bls_thread_pool_job_groups_started_total;
   assert.strictEqual(await verifier.verifySignatureSets(sets, {verifyOnMainThread: true}), true);
+  assert.strictEqual(verifier.metrics.lodestar_bls_thread_pool_job_groups_started_total, groups0, "priority path skips the queue");
   assert.strictEqual(verifier.verifySignatureSetsSync(sets), true);  // BlsSingleThreadVerifier semantics
   const wrongMsg = sets.map((s, k) => (k === 1 ? {...s, signingRoot: hex(v.jobs[0].sets[0].msg).map((b) => b ^ 1)} : s));
   assert.strictEqual(await verifier.verifySignatureSets(wrongMsg), false);
@@ -185,6 +187,17 @@ async function main() {
   assert.deepStrictEqual(await Promise.all([inflight, q1, q2]), [true, true, true]);
   assert.strictEqual(small.canAcceptWork(), true);
   await small.close();
+
+  // 5b. blsVerifyAllMultiThread (chain/options.ts:14): verifyOnMainThread calls
+  // join the queue like any other, and no CUs are reserved
+  const allMt = new BlsGpuVerifier({device: 0, blsVerifyAllMultiThread: true});
+  allMt.syncPubkeys(0, pk48);
+  assert.strictEqual(allMt.prioReserved, false);
+  const g0 = allMt.metrics.lodestar_bls_thread_pool_job_groups_started_total;
+  assert.strictEqual(await allMt.verifySignatureSets(sets, {verifyOnMainThread: true}), true);
+  assert.ok(allMt.metrics.lodestar_bls_thread_pool_job_groups_started_total > g0, "queued like any other call");
+  assert.strictEqual(await allMt.verifySignatureSets(wrongMsg, {verifyOnMainThread: true}), false);
+  await allMt.close();
 
   // 6. several devices owned by one process (SURVEY 8e): two contexts (both on
   // GPU 0 here) verify one batch split by job; partial Miller products, ONE

@@ -228,6 +228,15 @@ def test_async_verifier_like_reference_e2e():
             await pool.close()
         with pytest.raises(V.QueueError):
             await pool.verify_signature_sets(sets)
+        # blsVerifyAllMultiThread (chain/options.ts:14): verifyOnMainThread joins the queue
+        pool = V.BlsGpuVerifier(devices=(0,), bls_verify_all_multi_thread=True)
+        try:
+            jobs0 = pool.metrics["jobs_started"]
+            assert await pool.verify_signature_sets(sets, V.VerifySignatureOpts(verifyOnMainThread=True))
+            assert pool.metrics["jobs_started"] > jobs0
+            assert not pool.prio_reserved
+        finally:
+            await pool.close()
 
     asyncio.run(run())
 
