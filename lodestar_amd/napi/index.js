@@ -556,7 +556,50 @@ class BlsGpuVerifier {
   }
 }
 
+// BlsSingleThreadVerifier (chain/bls/singleThread.ts:7-46), which chain.ts:200-202
+// builds instead of the pool when blsVerifyAllMainThread is set: maybeBatch on
+// one device context, blocking the calling thread as blst does on the main
+// thread (addon.verifySync); canAcceptWork is always true.  Its pubkey table
+// is its own replica.
+class BlsGpuSingleThreadVerifier {
+  constructor({device = 0} = {}) {
+    this.ctx = addon.open(device, 0);
+    this.closed = false;
+    this.metrics = {lodestar_bls_aggregated_pubkeys_total: 0, lodestar_bls_thread_pool_main_thread_time_seconds: {count: 0, sum: 0}};
+  }
+
+  syncPubkeys(firstIndex, pubkeys48) {
+    addon.pubkeysSet(this.ctx, firstIndex, pubkeys48, 0);
+  }
+
+  pubkeysSet(firstIndex, bytes, format) {
+    addon.pubkeysSet(this.ctx, firstIndex, bytes, format);
+  }
+
+  async verifySignatureSets(sets) {
+    if (this.closed) throw new QueueError();
+    this.metrics.lodestar_bls_aggregated_pubkeys_total += aggregatedPubkeysCount(sets);
+    checkSets(sets); // getAggregatedPubkey's checks (utils.ts:5-16)
+    const t0 = now();
+    const res = addon.verifySync(this.ctx, encodeJobs([sets]));
+    const o = jobOutcome(res.results[0]);
+    if (!o.ok) throw o.error; // only runs without exceptions are timed, as in the reference
+    observe(this.metrics.lodestar_bls_thread_pool_main_thread_time_seconds, (now() - t0) / 1e3);
+    return o.value;
+  }
+
+  async close() {
+    if (this.closed) return;
+    this.closed = true;
+    addon.close(this.ctx);
+  }
+
+  canAcceptWork() {
+    return true;
+  }
+}
+
 module.exports = {
-  addon, BlsGpuVerifier, QueueError, sourceHash, checkBuildId, chunkifyMaximizeChunkSize, encodeJobs, checkSets, shardJobs, jobWork,
+  addon, BlsGpuVerifier, BlsGpuSingleThreadVerifier, QueueError, sourceHash, checkBuildId, chunkifyMaximizeChunkSize, encodeJobs, checkSets, shardJobs, jobWork,
   MAX_BUFFERED_SIGS, MAX_BUFFER_WAIT_MS, MAX_JOBS_CAN_ACCEPT_WORK, SHARD_MIN_SETS, PRIORITY_CUS, RESERVED_CAP,
 };

@@ -8,7 +8,7 @@ const assert = require("assert");
 const fs = require("fs");
 const path = require("path");
 
-const {addon, BlsGpuVerifier, QueueError} = require(path.join(__dirname, "..", "..", "lodestar_amd", "napi"));
+const {addon, BlsGpuVerifier, BlsGpuSingleThreadVerifier, QueueError} = require(path.join(__dirname, "..", "..", "lodestar_amd", "napi"));
 const golden = path.join(__dirname, "..", "golden");
 const hex = (s) => Uint8Array.from(Buffer.from(s.replace(/^0x/, ""), "hex"));
 
@@ -198,6 +198,17 @@ async function main() {
   assert.ok(allMt.metrics.lodestar_bls_thread_pool_job_groups_started_total > g0, "queued like any other call");
   assert.strictEqual(await allMt.verifySignatureSets(wrongMsg, {verifyOnMainThread: true}), false);
   await allMt.close();
+
+  // 5c. BlsSingleThreadVerifier (blsVerifyAllMainThread, chain.ts:200-202)
+  const single = new BlsGpuSingleThreadVerifier({device: 0});
+  single.syncPubkeys(0, pk48);
+  assert.strictEqual(single.canAcceptWork(), true);
+  assert.strictEqual(await single.verifySignatureSets(sets), true);
+  assert.strictEqual(await single.verifySignatureSets(wrongMsg), false);
+  await assert.rejects(single.verifySignatureSets([]), /Empty signature set/);
+  assert.strictEqual(single.metrics.lodestar_bls_thread_pool_main_thread_time_seconds.count, 2);
+  await single.close();
+  await assert.rejects(single.verifySignatureSets(sets), QueueError);
 
   // 6. several devices owned by one process (SURVEY 8e): two contexts (both on
   // GPU 0 here) verify one batch split by job; partial Miller products, ONE
