@@ -602,6 +602,43 @@ class BlsGpuVerifier:
             t.join()
 
 
+class BlsGpuSingleThreadVerifier:
+    """BlsSingleThreadVerifier (chain/bls/singleThread.ts:7-46), which
+    chain.ts:200-202 builds instead of the pool when blsVerifyAllMainThread is
+    set: maybeBatch on one device context in the calling thread (the event loop
+    waits, as it does for blst on the main thread); can_accept_work() is always
+    True.  Its pubkey table is its own replica."""
+
+    def __init__(self, device: int = 0, metrics: dict | None = None):
+        self.device = native.Device(device)
+        self.table = PubkeyTable([self.device])
+        self.metrics = metrics if metrics is not None else {"aggregated_pubkeys_total": 0, "main_thread_time_s": 0.0,
+                                                            "main_thread_calls": 0}
+        self._closed = False
+
+    async def verify_signature_sets(self, sets: list[ISignatureSet], opts: VerifySignatureOpts | None = None) -> bool:
+        if self._closed:
+            raise QueueError(QueueErrorCode.QUEUE_ABORTED)
+        self.metrics["aggregated_pubkeys_total"] += get_aggregated_pubkeys_count(sets)
+        check_sets(sets)  # getAggregatedPubkey's checks (utils.ts:5-16)
+        t0 = time.perf_counter()
+        jr, _ = self.device.verify(encode_jobs([sets]), want_set_codes=False)
+        r = BlsGpuVerifier._verdict(int(jr[0]))
+        if isinstance(r, Exception):
+            raise r  # only runs without exceptions are timed, as in the reference
+        self.metrics["main_thread_time_s"] += time.perf_counter() - t0
+        self.metrics["main_thread_calls"] += 1
+        return r
+
+    def can_accept_work(self) -> bool:
+        return True
+
+    async def close(self):
+        if not self._closed:
+            self._closed = True
+            self.device.close()
+
+
 async def reject_first_invalid_resolve_all_valid(is_valid_awaitables) -> dict:
     """chain/blocks/verifyBlocksSignatures.ts:69-89: resolves {"allValid": False,
     "index": i} at the first False to arrive, {"allValid": True} when all are

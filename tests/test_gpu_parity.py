@@ -228,6 +228,20 @@ def test_async_verifier_like_reference_e2e():
             await pool.close()
         with pytest.raises(V.QueueError):
             await pool.verify_signature_sets(sets)
+        # BlsSingleThreadVerifier (blsVerifyAllMainThread, chain.ts:200-202)
+        single = V.BlsGpuSingleThreadVerifier(0)
+        try:
+            assert single.can_accept_work()
+            assert await single.verify_signature_sets(sets)
+            wrong = [V.create_single_signature_set_from_components(sets[0].pubkey, sets[1].signingRoot, sets[0].signature)]
+            assert not await single.verify_signature_sets(wrong)
+            with pytest.raises(V.BlsError, match="Empty signature set"):
+                await single.verify_signature_sets([])
+            assert single.metrics["main_thread_calls"] == 2
+        finally:
+            await single.close()
+        with pytest.raises(V.QueueError):
+            await single.verify_signature_sets(sets)
         # blsVerifyAllMultiThread (chain/options.ts:14): verifyOnMainThread joins the queue
         pool = V.BlsGpuVerifier(devices=(0,), bls_verify_all_multi_thread=True)
         try:
