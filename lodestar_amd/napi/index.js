@@ -231,6 +231,8 @@ function newMetrics() {
     lodestar_bls_thread_pool_latency_to_worker: hist(),
     lodestar_bls_thread_pool_latency_from_worker: hist(),
     lodestar_bls_worker_thread_time_per_sigset_seconds: hist(),
+    // verifyOnMainThread calls (mainThreadDurationInThreadPool, multithread/index.ts:156-167)
+    lodestar_bls_thread_pool_main_thread_time_seconds: hist(),
   };
 }
 
@@ -337,6 +339,7 @@ class BlsGpuVerifier {
       const pending = addon.verify(this.prio, batch);
       this.lastPriorityIssue = {encodeMs: t1 - t0, queueMs: now() - t1};
       const res = await pending;
+      observe(this.metrics.lodestar_bls_thread_pool_main_thread_time_seconds, (now() - t0) / 1e3);
       this.recordWork([{sets}], res);
       const o = jobOutcome(res.results[0]);
       if (!o.ok) throw o.error;

@@ -495,6 +495,9 @@ class BlsGpuVerifier:
                 t0 = time.perf_counter()
                 jr, _ = self.prio.verify(arrays, want_set_codes=False)
                 self._record(self.prio.last_stats, time.perf_counter() - t0)
+                # mainThreadDurationInThreadPool (multithread/index.ts:156-167)
+                self.metrics["main_thread_time_s"] += time.perf_counter() - t0
+                self.metrics["main_thread_calls"] += 1
         except Exception as e:  # noqa: BLE001 -- a device error rejects the call
             return e
         return self._verdict(int(jr[0]))
@@ -694,6 +697,8 @@ def _new_metrics() -> dict:
     return {
         "aggregated_pubkeys_total": 0,
         "jobs_started": 0,
+        "main_thread_time_s": 0.0,
+        "main_thread_calls": 0,
         "sets_started": 0,
         "batch_retries": 0,
         "batch_sigs_success": 0,

@@ -96,6 +96,7 @@ async function main() {
   const groups0 = verifier.metrics.lodestar_bls_thread_pool_job_groups_started_total;
   assert.strictEqual(await verifier.verifySignatureSets(sets, {verifyOnMainThread: true}), true);
   assert.strictEqual(verifier.metrics.lodestar_bls_thread_pool_job_groups_started_total, groups0, "priority path skips the queue");
+  assert.ok(verifier.metrics.lodestar_bls_thread_pool_main_thread_time_seconds.count >= 1, "main-thread duration series");
   assert.strictEqual(verifier.verifySignatureSetsSync(sets), true);  // BlsSingleThreadVerifier semantics
   const wrongMsg = sets.map((s, k) => (k === 1 ? {...s, signingRoot: hex(v.jobs[0].sets[0].msg).map((b) => b ^ 1)} : s));
   assert.strictEqual(await verifier.verifySignatureSets(wrongMsg), false);

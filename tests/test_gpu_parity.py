@@ -214,6 +214,7 @@ def test_async_verifier_like_reference_e2e():
             assert await pool.verify_signature_sets(sets)
             assert await pool.verify_signature_sets(sets, V.VerifySignatureOpts(batchable=True))
             assert await pool.verify_signature_sets(sets, V.VerifySignatureOpts(verifyOnMainThread=True))
+            assert pool.metrics["main_thread_calls"] == 1  # mainThreadDurationInThreadPool
             good = [pool.verify_signature_sets(sets, V.VerifySignatureOpts(batchable=True)) for _ in range(8)]
             bad_set = V.create_single_signature_set_from_components(sets[0].pubkey, sets[0].signingRoot, bytes(32))
             bad = pool.verify_signature_sets([bad_set], V.VerifySignatureOpts(batchable=True))
