@@ -389,6 +389,50 @@ def shard_projection(d, torch, dev, arrays_host: dict, worlds=(2, 4, 8), reps: i
     return out
 
 
+def reserved_device(d, gpu, torch, dev, darr, arrays_host: dict, reps: int = 5):
+    """The bulk pace of a device whose bulk context leaves 32 CUs to a
+    verifyOnMainThread priority context (bgv_cfg.cu_split = -32; the pools'
+    device 0 on a multi-device node, and on one device when asked): C4 and the
+    heaviest C4/8 shard (bgv_partial) on a reserved context against the same
+    batches on the unreserved one, medians of `reps`.  cap_at_shard is the
+    RESERVED_CAP the shard weighting should use (lodestar_amd/napi/reserved_cap.json)."""
+    from lodestar_amd import native
+    from lodestar_amd.dist import RESERVED_CAP, batch_job_work, select_jobs, shard_jobs
+    work = batch_job_work(arrays_host)
+    ids = max(shard_jobs(work, 8), key=lambda s: sum(work[j] for j in s))
+    sub = to_device(select_jobs(arrays_host, ids), torch, dev)
+    sub["scalars"] = None
+
+    def med(ctx):
+        c4, sh = [], []
+        for k in range(reps + 1):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            jr, _ = ctx.verify(darr, on_device=True, want_set_codes=False)
+            t2 = time.perf_counter()
+            _, _, _, ok = ctx.partial(sub, on_device=True)
+            t3 = time.perf_counter()
+            assert (jr == 1).all() and ok
+            if k:
+                c4.append((t2 - t1) * 1e3)
+                sh.append((t3 - t2) * 1e3)
+        return float(np.median(c4)), float(np.median(sh))
+
+    dr = native.Device(gpu, cu_split=-32)
+    try:
+        dr.gen_keys(0, N_VALIDATORS, SEED)
+        free_c4, free_sh = med(d)
+        res_c4, res_sh = med(dr)
+    finally:
+        dr.close()
+    return {"cu_split": -32, "c4_ms": round(res_c4, 3), "c4_unreserved_ms": round(free_c4, 3),
+            "c4_over_8_ms": round(res_sh, 3), "c4_over_8_unreserved_ms": round(free_sh, 3),
+            "sets_per_s": round(arrays_host["n_sets"] / res_c4 * 1e3, 1),
+            "cap_at_c4": round(free_c4 / res_c4, 4), "cap_at_shard": round(free_sh / res_sh, 4),
+            "reserved_cap_in_use": RESERVED_CAP,
+            "note": "pool default: reserved only with >= 2 devices (device 0); a one-device pool reserves nothing unless priorityCus asks"}
+
+
 def timed_steps(step, dist, coll_dev, torch, steps: int, warmup: int):
     """W untimed + K timed steps between barriers; the max elapsed over ranks"""
     for _ in range(warmup):
@@ -554,6 +598,7 @@ def main():
         legs["mixed_sizes"] = mixed_sizes(d, darr)
         if world == 1:
             legs["strong_shard_projection"] = shard_projection(d, torch, dev, host)
+            legs["reserved_device"] = reserved_device(d, gpu, torch, dev, darr, host)
 
     # roofline (INT32 VALU): algorithmic Fp-mul per set x sets / the stage's
     # HIP-event time in the timed steps, for every stage; the dominant kernel

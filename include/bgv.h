@@ -299,6 +299,14 @@ int bgv_gen_sign(bgv_ctx* ctx, const bgv_batch* batch, uint8_t* sigs_out192);
  * add), -a, [a+b unreduced, b-a] (lazy add / sub pair).  Host pointers. */
 #define BGV_FP_OPS_N 13
 int bgv_debug_fp_ops(bgv_ctx* ctx, const uint32_t* ab_in, uint32_t n, uint32_t* out);
+/* The signature decode of Signature.fromBytes(sig, affine, true) without its
+ * subgroup check (tests only; maybeBatch.ts:23,36): sigs192[i] holds a 96-byte
+ * compressed or 192-byte uncompressed encoding (sig_len[i]); out192[i] gets the
+ * affine point as x.c0 || x.c1 || y.c0 || y.c1, 48 big-endian bytes each
+ * (zero for the identity or a failed decode), codes[i] the BGV set code.
+ * Host pointers. */
+int bgv_debug_g2_decode(bgv_ctx* ctx, const uint8_t* sigs192, const uint32_t* sig_len, uint32_t n, uint8_t* out192,
+                        int32_t* codes);
 
 /* ---- microbenchmarks for the roofline ------------------------ */
 /* Montgomery Fp-mul throughput: `lanes` independent chains of `iters`

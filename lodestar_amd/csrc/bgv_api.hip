@@ -206,9 +206,44 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(BGV_E_NO_DEVICE, "no HIP device visible");
   if (device < 0 || device >= n) return fail(BGV_E_NO_DEVICE, "device %d out of range (%d devices)", device, n);
   HIPCHK(hipSetDevice(device));
+  // CU partition between a priority context (the |N| highest CU ids) and the
+  // bulk contexts (the rest): a single set's few waves then never queue
+  // behind a resident bulk batch (k_hash alone holds two waves on every SIMD
+  // for ~16 ms at C4).  Streams with a CU mask take no priority.  Mask bit i
+  // is CU i / 8 of XCC i % 8, in shader engine (i / 8) % 4
+  // (tools/cu_mask_probe.hip, probed on MI355X: 8 XCCs x 32 CUs), and an XCC
+  // left without any bit runs on all of its CUs, so N must be a multiple of
+  // the XCC count: the highest 8k ids then take k CUs from every XCC (32: one
+  // per SE).  Any other layout is refused rather than half-isolated.
+  // Workgroups go round-robin over the SEs, so the bulk side runs at the pace
+  // of an SE that lost a CU: C4 +13% for 8, 16 or 32 reserved CUs alike
+  // (profiles/r05h_cu_split.txt).
+  std::vector<uint32_t> mask;
+  if (k.cu_split != 0) {
+    int n_cu = 0, n_xcc = 0;
+    HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
+    if (hipDeviceGetAttribute(&n_xcc, hipDeviceAttributeNumberOfXccs, device) != hipSuccess) n_xcc = 0;
+    const int reserve = k.cu_split > 0 ? k.cu_split : -k.cu_split;
+    if (n_xcc != 8 || n_cu != 256)
+      return fail(BGV_E_INVALID_ARG, "bgv_cfg.cu_split %d: the CU-mask layout is probed for 8 XCCs x 32 CUs (device: %d XCCs, %d CUs)",
+                  k.cu_split, n_xcc, n_cu);
+    if (reserve % n_xcc != 0)
+      return fail(BGV_E_INVALID_ARG, "bgv_cfg.cu_split %d: |N| must be a multiple of the %d XCCs (an XCC without a mask bit runs on all its CUs)",
+                  k.cu_split, n_xcc);
+    mask.assign((size_t)(n_cu + 31) / 32, 0u);
+    for (int cu = 0; cu < n_cu; cu++) {
+      const bool reserved = cu >= n_cu - reserve;
+      if (reserved == (k.cu_split > 0)) mask[cu / 32] |= 1u << (cu % 32);
+    }
+  }
   bgv_ctx* c = new bgv_ctx();
   c->device = device;
   c->cfg = k;
+  // on a failure below, the streams and events made so far go with the context
+  struct guard_t {
+    bgv_ctx*& c;
+    ~guard_t() { if (c) bgv_close(c); }
+  } guard{c};
   // hash -> set-pair Miller is the critical path: its stream (and the pubkey
   // stream feeding it) get the highest priority, signature decode/scaling the
   // lowest (it only feeds the signature tree and the 1 pair per job)
@@ -220,25 +255,6 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
     HIPCHK(hipStreamCreateWithPriority(&c->st_pk, hipStreamNonBlocking, prio_hi));
     HIPCHK(hipStreamCreateWithPriority(&c->st_chk, hipStreamNonBlocking, prio_lo));
   } else {
-    // CU partition between a priority context (the |N| highest CU ids) and the
-    // bulk contexts (the rest): a single set's few waves then never queue
-    // behind a resident bulk batch (k_hash alone holds two waves on every SIMD
-    // for ~16 ms at C4).  Streams with a CU mask take no priority.  Mask bit i
-    // is CU i / 8 of XCC i % 8, in shader engine (i / 8) % 4
-    // (tools/cu_mask_probe.hip), and an XCC left without any bit runs on all of
-    // its CUs, so the highest 8k ids take k CUs from every XCC (32: one per
-    // SE).  Workgroups go round-robin over the SEs, so the bulk side runs at
-    // the pace of an SE that lost a CU: C4 +13% for 8, 16 or 32 reserved CUs
-    // alike (profiles/r05h_cu_split.txt), and the priority side gets 32.
-    int n_cu = 0;
-    HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
-    const int reserve = k.cu_split > 0 ? k.cu_split : -k.cu_split;
-    if (n_cu <= reserve) return fail(BGV_E_INVALID_ARG, "bgv_cfg.cu_split %d with %d CUs", k.cu_split, n_cu);
-    std::vector<uint32_t> mask((size_t)(n_cu + 31) / 32, 0u);
-    for (int cu = 0; cu < n_cu; cu++) {
-      const bool reserved = cu >= n_cu - reserve;
-      if (reserved == (k.cu_split > 0)) mask[cu / 32] |= 1u << (cu % 32);
-    }
     hipStream_t* sts[4] = {&c->st, &c->st_hash, &c->st_pk, &c->st_chk};
     for (hipStream_t* p : sts) HIPCHK(hipExtStreamCreateWithCUMask(p, (uint32_t)mask.size(), mask.data()));
   }
@@ -253,6 +269,7 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
   HIPCHK(hipEventCreateWithFlags(&c->ev_maps, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&c->ev_chk, hipEventDisableTiming));
   *out = c;
+  c = nullptr;  // owned by the caller now
   return BGV_OK;
 }
 
@@ -669,21 +686,9 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
     // set has its own Miller value, which the per-job fold relies on)
     else if (d.miller_coop) d.pairs_per_item = 1;
   }
-  // fixed-argument lines (pairing.h miller_lines): the G2 half of the one-lane
-  // Miller loop moves to the hash stream, phase 1 (C4 40.4 -> 39.5 ms); with
-  // one pair per item it loses (C4/2 26.4 -> 28.5 ms)
-  d.lines = (uint32_t)(!d.split && !d.miller_coop && (k.lines >= 0 ? k.lines : d.pairs_per_item == 2));
-  // the lines take 3 x 68 Fp2 = 19.6 KB per set (1.97 GB at C4, 2.6 GB at the
-  // Node pool's 2^17-set batch cap): kept only while a quarter of the free HBM
-  // covers them, else the loop recomputes them (miller_loop2, same values)
-  if (d.lines) {
-    const size_t need = (size_t)3 * MILLER_STEPS * n * sizeof(fp2_t);
-    size_t free_b = 0, total_b = 0;
-    if (need > c->lines.cap * sizeof(fp2_t) &&
-        (hipMemGetInfo(&free_b, &total_b) != hipSuccess || need > free_b / 4))
-      d.lines = 0;
-  }
   d.job_lanes = k.job_lanes ? (uint32_t)k.job_lanes : 36u;
+  // the scalars are allocated before the line decision below, so a line buffer
+  // that ensure_or_release_lines gives up here is seen by that decision
   if (b->scalars && !b->on_device) {
     // staged with the other host arrays above
   } else if (b->scalars) {
@@ -697,6 +702,20 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
     launch_gen_scalars(c->st, kn, kn + 8, c->scalars.p, n);
     HIPCHK(hipGetLastError());
     d.scalars = c->scalars.p;
+  }
+  // fixed-argument lines (pairing.h miller_lines): the G2 half of the one-lane
+  // Miller loop moves to the hash stream, phase 1 (C4 40.4 -> 39.5 ms); with
+  // one pair per item it loses (C4/2 26.4 -> 28.5 ms)
+  d.lines = (uint32_t)(!d.split && !d.miller_coop && (k.lines >= 0 ? k.lines : d.pairs_per_item == 2));
+  // the lines take 3 x 68 Fp2 = 19.6 KB per set (1.97 GB at C4, 2.6 GB at the
+  // Node pool's 2^17-set batch cap): kept only while a quarter of the free HBM
+  // covers them, else the loop recomputes them (miller_loop2, same values)
+  if (d.lines) {
+    const size_t need = (size_t)3 * MILLER_STEPS * n * sizeof(fp2_t);
+    size_t free_b = 0, total_b = 0;
+    if (need > c->lines.cap * sizeof(fp2_t) &&
+        (hipMemGetInfo(&free_b, &total_b) != hipSuccess || need > free_b / 4))
+      d.lines = 0;
   }
   return 0;
 }
@@ -1164,6 +1183,28 @@ int bgv_debug_fp_ops(bgv_ctx* c, const uint32_t* ab_in, uint32_t n, uint32_t* ou
   launch_fp_ops(c->st, d_ab, d_out, n);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(out, d_out, (size_t)n * BGV_FP_OPS_N * sizeof(fp_t), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return BGV_OK;
+}
+
+int bgv_debug_g2_decode(bgv_ctx* c, const uint8_t* sigs192, const uint32_t* sig_len, uint32_t n, uint8_t* out192,
+                        int32_t* codes) {
+  if (!c || (n && (!sigs192 || !sig_len || !out192 || !codes))) return fail(BGV_E_INVALID_ARG, "null argument");
+  if (n > (1u << 20)) return fail(BGV_E_INVALID_ARG, "at most 2^20 encodings");
+  if (!n) return BGV_OK;
+  HIPCHK(hipSetDevice(c->device));
+  const size_t bytes = (size_t)n * (192 + 4 + 192 + 4);
+  if (int r = c->dbg_out.ensure(bytes)) return r;
+  uint8_t* d_sig = c->dbg_out.p;
+  uint32_t* d_len = (uint32_t*)(d_sig + (size_t)n * 192);
+  uint8_t* d_out = (uint8_t*)(d_len + n);
+  int32_t* d_code = (int32_t*)(d_out + (size_t)n * 192);
+  HIPCHK(hipMemcpyAsync(d_sig, sigs192, (size_t)n * 192, hipMemcpyHostToDevice, c->st));
+  HIPCHK(hipMemcpyAsync(d_len, sig_len, (size_t)n * 4, hipMemcpyHostToDevice, c->st));
+  launch_g2_decode_dbg(c->st, d_sig, d_len, d_out, d_code, n);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out192, d_out, (size_t)n * 192, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipMemcpyAsync(codes, d_code, (size_t)n * 4, hipMemcpyDeviceToHost, c->st));
   HIPCHK(hipStreamSynchronize(c->st));
   return BGV_OK;
 }

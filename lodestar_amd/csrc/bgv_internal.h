@@ -150,6 +150,8 @@ void launch_fp12_convert(hipStream_t st, const fp12_t* in, fp12_t* out, uint32_t
 void launch_gen_keys(hipStream_t st, g1a* table, uint32_t* sk, uint32_t first, uint32_t n, uint64_t seed);
 void launch_gen_sign(hipStream_t st, const dev_batch& b, const uint32_t* sk, uint8_t* out);
 void launch_fp_ops(hipStream_t st, const fp_t* ab, fp_t* out, uint32_t n);
+void launch_g2_decode_dbg(hipStream_t st, const uint8_t* sigs192, const uint32_t* sig_len, uint8_t* out192, int32_t* codes,
+                         uint32_t n);
 void launch_bench_fpmul(hipStream_t st, fp_t* io, uint32_t lanes, uint32_t iters);
 void launch_gen_scalars(hipStream_t st, const uint32_t key[8], const uint32_t nonce[3], uint64_t* out, uint32_t n);
 void launch_bench_mad(hipStream_t st, uint64_t* io, uint32_t lanes, uint32_t iters);

@@ -1076,6 +1076,33 @@ __global__ void BGV_BULK k_fp_ops(const fp_t* ab, fp_t* out, uint32_t n) {
   fp_addnr_sub(r0, a, b, r1, b, a); o[11] = r0; o[12] = r1;
 }
 
+// bgv_debug_g2_decode: Signature.fromBytes' decode alone (g2_decompress /
+// g2_deserialize, no subgroup check) on host-chosen encodings, so a test can
+// put lanes that take the y.c1 = 0 / y.c0 = 0 arms of fp2_sqrt and
+// fp2_lex_largest beside ordinary lanes of one wave and compare every decoded
+// point (an off-subgroup point is zeroed by the verify path's k_sig).
+__global__ void BGV_BULK k_g2_decode_dbg(const uint8_t* sigs192, const uint32_t* sig_len, uint8_t* out192, int32_t* codes,
+                                        uint32_t n) {
+  const uint32_t i = gtid();
+  if (i >= n) return;
+  const uint32_t len = sig_len[i];
+  const uint8_t* s = sigs192 + 192u * i;
+  g2a a;
+  bool inf = false;
+  int32_t code;
+  if (len == 96u) code = g2_decompress(a, inf, s);
+  else if (len == 192u) code = g2_deserialize(a, inf, s);
+  else code = C_INVALID_SIZE;
+  if (code != C_OK || inf) { a.x = fp2_zero(); a.y = fp2_zero(); }
+  const fp_t* c[4] = {&a.x.c0, &a.x.c1, &a.y.c0, &a.y.c1};
+  for (int k = 0; k < 4; k++) {
+    fp_t t;
+    fp_from_mont(t, *c[k]);
+    fp_to_be48(out192 + 192u * i + 48 * k, t);
+  }
+  codes[i] = code;
+}
+
 // ========================================================= microbenchmarks
 __global__ void __launch_bounds__(256) k_bench_fpmul(fp_t* io, uint32_t iters) {
   const uint32_t i = gtid();
@@ -1306,6 +1333,10 @@ void launch_gen_keys(hipStream_t st, g1a* table, uint32_t* sk, uint32_t first, u
 }
 void launch_gen_sign(hipStream_t st, const dev_batch& b, const uint32_t* sk, uint8_t* out) {
   BGV_LAUNCH(k_gen_sign, b.n_sets, b, sk, out);
+}
+void launch_g2_decode_dbg(hipStream_t st, const uint8_t* sigs192, const uint32_t* sig_len, uint8_t* out192, int32_t* codes,
+                         uint32_t n) {
+  BGV_LAUNCH(k_g2_decode_dbg, n, sigs192, sig_len, out192, codes, n);
 }
 void launch_fp_ops(hipStream_t st, const fp_t* ab, fp_t* out, uint32_t n) {
   if (n) hipLaunchKernelGGL(k_fp_ops, dim3((n + 63u) / 64u), dim3(64), 0, st, ab, out, n);

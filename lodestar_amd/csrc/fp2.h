@@ -162,10 +162,16 @@ BGV_HD uint32_t fp2_sgn0(const fp2_t& a) {
   return s0 | (z0 & s1);
 }
 
-// ZCash serialization sign: c1 decides unless zero, then c0
+// ZCash serialization sign: c1 decides unless zero, then c0.  Both signs are
+// computed and selected: no data-dependent return.  gfx950 miscompiled the
+// early-return form of this choice under a divergent exec mask on the
+// digit-form branch (overlapping spill reloads of the two arms: one signature
+// in 66,640 decoded to -y); test_gpu_decode_mixed.py puts
+// y.c1 = 0 and y.c0 = 0 lanes beside ordinary ones in one wave.
 BGV_HD bool fp2_lex_largest(const fp2_t& a) {
-  if (!fp_is_zero(a.c1)) return fp_lex_largest(a.c1);
-  return fp_lex_largest(a.c0);
+  const bool z1 = fp_is_zero(a.c1);
+  const bool l1 = fp_lex_largest(a.c1), l0 = fp_lex_largest(a.c0);
+  return z1 ? l0 : l1;
 }
 
 // Square root in Fp2 through two Fp exponentiations (p = 3 mod 4):
@@ -194,27 +200,28 @@ BGV_NI void fp2_sqrt_tail(fp2_t& r, const fp2_t& a, const fp_t& d) {
 }
 
 // a1 == 0 is handled directly in Fp.  Returns false iff a is a non-square.
+// One exit and no data-dependent return (the arms diverge inside a wave when
+// y.c1 = 0 lanes sit beside ordinary ones; see fp2_lex_largest).
 BGV_NI bool fp2_sqrt(fp2_t& r, const fp2_t& a) {
+  bool ok = true;
   if (fp_is_zero(a.c1)) {
-    fp_t s;
-    if (fp_sqrt(s, a.c0)) {
-      r.c0 = s;
-      fp_set_zero(r.c1);
-      return true;
-    }
-    fp_t na;
-    fp_neg(na, a.c0);
-    // -1 is a non-residue, so -a0 is a square here: x = sqrt(-a0) * i
-    fp_sqrt(s, na);
-    fp_set_zero(r.c0);
-    r.c1 = s;
-    return true;
+    // s = a0^((p+1)/4) squares to a0 a0^((p-1)/2) = +-a0.  For a non-residue
+    // a0, -a0 is a square (-1 is a non-residue) and its root
+    // (-a0)^((p+1)/4) = -s ((p+1)/4 is odd): x = -s i
+    fp_t s, ns, z;
+    const bool re = fp_sqrt(s, a.c0);
+    fp_neg(ns, s);
+    fp_set_zero(z);
+    fp_select(r.c0, re, s, z);
+    fp_select(r.c1, re, z, ns);
+  } else {
+    fp_t n, d;
+    fp2_norm(n, a);
+    ok = fp_sqrt(d, n);
+    if (ok) fp2_sqrt_tail(r, a, d);
+    else r = a;
   }
-  fp_t n, d;
-  fp2_norm(n, a);
-  if (!fp_sqrt(d, n)) return false;
-  fp2_sqrt_tail(r, a, d);
-  return true;
+  return ok;
 }
 
 // a is a square in Fp2 iff its norm is a square in Fp

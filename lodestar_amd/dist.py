@@ -18,6 +18,9 @@ verdicts are then all-gathered so every rank holds the whole batch's.
 """
 from __future__ import annotations
 
+import json
+import os
+
 import numpy as np
 
 PARTIAL_BYTES = 576
@@ -69,10 +72,13 @@ def shard_jobs(job_weights, world: int, caps=None) -> list[list[int]]:
 
 
 # throughput of a device whose bulk context reserves CUs for a priority context
-# (bgv_cfg.cu_split < 0): workgroups go round-robin over the shader engines, so
-# the bulk context runs at the pace of an engine with 7 of its 8 CUs
-# (C4 36.8 -> 41.7 ms)
-RESERVED_CAP = 7.0 / 8.0
+# (bgv_cfg.cu_split < 0), relative to an unreserved one, at the 8-GPU shard
+# size: workgroups go round-robin over the shader engines, so the bulk context
+# runs at the pace of an engine that lost a CU, and the mid-size chains pay more
+# than C4 (12,544 sets 9.55 -> 11.73 ms; C4 36.8 -> 41.7 ms).
+# One value for both bindings: napi/reserved_cap.json (index.js reads it too).
+with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "napi", "reserved_cap.json")) as _f:
+    RESERVED_CAP = float(json.load(_f)["RESERVED_CAP"])
 
 
 def shard_balance(job_weights, shards) -> float:

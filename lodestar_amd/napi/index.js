@@ -79,10 +79,12 @@ const MAX_JOBS_CAN_ACCEPT_WORK = 512; // multithread/index.ts:62
 const MAX_SETS_PER_DEVICE_BATCH = 1 << 17;
 const now = () => Number(process.hrtime.bigint()) / 1e6;
 // CUs of the first device kept for verifyOnMainThread (bgv_cfg.cu_split): the top 32 ids are one CU of every
-// shader engine, and any reservation costs that device's bulk context ~13% (DESIGN.md §3), so the priority side
-// takes 32 rather than 8
+// shader engine, and any reservation costs that device's bulk context ~13% at C4 and ~20% at the 8-GPU shard size
+// (DESIGN.md §3), so the priority side takes 32 rather than 8.  The default reserves them only on a pool of two or
+// more devices, where sharded batches give device 0 a RESERVED_CAP-weighted share; a one-device pool keeps the
+// whole chip for its bulk batches unless priorityCus asks for the split.
 const PRIORITY_CUS = 32;
-const RESERVED_CAP = 7 / 8; // dist.py RESERVED_CAP: bulk pace of a device with reserved CUs
+const RESERVED_CAP = require("./reserved_cap.json").RESERVED_CAP; // dist.py RESERVED_CAP: bulk pace of a device with reserved CUs
 // a device batch of at least this many sets (and >= 2 jobs) is split by job
 // over the idle devices (partial Miller products, ONE combined final
 // exponentiation); smaller batches run whole on one device while the other
@@ -246,18 +248,21 @@ class BlsGpuVerifier {
   // (chain/chain.ts:199-202 constructs one verifier per node); every context
   // holds a replica of the pubkey table
   // priorityCus: CUs of the first device reserved for verifyOnMainThread
-  // (bgv_cfg.cu_split): a priority context runs there, the bulk context of
-  // that device leaves them free (~13% of its throughput whatever the count:
-  // the shader engines that lost a CU set the pace; sharded batches give that
-  // device a proportionally smaller shard); 0 disables the reservation (the
+  // (bgv_cfg.cu_split, a multiple of 8): a priority context runs there, the
+  // bulk context of that device leaves them free (~13-20% of its throughput
+  // whatever the count: the shader engines that lost a CU set the pace;
+  // sharded batches give that device a RESERVED_CAP-weighted shard).  Default:
+  // PRIORITY_CUS on a pool of two or more devices, 0 on one device (the
   // priority context then shares every CU)
   // blsVerifyAllMultiThread (chain/options.ts:14, multithread/index.ts:124): verifyOnMainThread
-  // calls join the pool's queue like any other; no CUs are then reserved
+  // calls join the pool's queue like any other; no CUs are then reserved and
+  // no priority context is opened
   constructor({device = 0, devices = null, maxSetsPerDeviceBatch = MAX_SETS_PER_DEVICE_BATCH, shardMinSets = SHARD_MIN_SETS,
-    priorityCus = PRIORITY_CUS, blsVerifyAllMultiThread = false} = {}) {
+    priorityCus = null, blsVerifyAllMultiThread = false} = {}) {
+    const ids = devices && devices.length ? devices : [device];
+    if (priorityCus === null || priorityCus === undefined) priorityCus = ids.length > 1 ? PRIORITY_CUS : 0;
     if (blsVerifyAllMultiThread) priorityCus = 0;
     this.blsVerifyAllMultiThread = blsVerifyAllMultiThread;
-    const ids = devices && devices.length ? devices : [device];
     // every device batch holds a libuv pool thread (napi_async_work); the pool
     // size is read once, when the pool first starts, so the launcher must set
     // UV_THREADPOOL_SIZE before Node runs any async work (INTEGRATION.md 4)
@@ -273,9 +278,12 @@ class BlsGpuVerifier {
     this.ctxs = ids.map((d, k) => addon.open(d, k === 0 && priorityCus > 0 ? -priorityCus : 0));
     this.ctx = this.ctxs[0];
     // verifyOnMainThread's own context (with its own table replica and mutex):
-    // it never waits for a bulk batch's context lock or, with priorityCus, its waves
-    this.prio = addon.open(ids[0], priorityCus > 0 ? priorityCus : 0);
+    // it never waits for a bulk batch's context lock or, with priorityCus, its
+    // waves.  Under blsVerifyAllMultiThread nothing uses it: the blocking
+    // verifySignatureSetsSync then runs on the first bulk context
+    this.prio = blsVerifyAllMultiThread ? null : addon.open(ids[0], priorityCus > 0 ? priorityCus : 0);
     this.prioReserved = priorityCus > 0;
+    this.priorityCus = priorityCus;
     this.prioBusy = 0;
     this.idle = ids.map(() => true);
     this.maxSetsPerDeviceBatch = maxSetsPerDeviceBatch;
@@ -301,7 +309,11 @@ class BlsGpuVerifier {
 
   // rows in either format (0: 48-byte compressed, 1: 96-byte uncompressed) into every replica
   pubkeysSet(firstIndex, bytes, format) {
-    for (const c of this.ctxs.concat([this.prio])) addon.pubkeysSet(c, firstIndex, bytes, format);
+    for (const c of this.allContexts()) addon.pubkeysSet(c, firstIndex, bytes, format);
+  }
+
+  allContexts() {
+    return this.prio ? this.ctxs.concat([this.prio]) : this.ctxs.slice();
   }
 
   // multithread/index.ts:143-149.  A queued job joins the next device batch,
@@ -332,19 +344,21 @@ class BlsGpuVerifier {
   // It bypasses the buffer, the job queue and the bulk contexts' locks.
   async verifyPriority(sets) {
     this.prioBusy++;
+    const t0 = now();
     try {
-      const t0 = now();
       const batch = encodeJobs([sets]);
       const t1 = now();
       const pending = addon.verify(this.prio, batch);
       this.lastPriorityIssue = {encodeMs: t1 - t0, queueMs: now() - t1};
       const res = await pending;
-      observe(this.metrics.lodestar_bls_thread_pool_main_thread_time_seconds, (now() - t0) / 1e3);
       this.recordWork([{sets}], res);
       const o = jobOutcome(res.results[0]);
       if (!o.ok) throw o.error;
       return o.value;
     } finally {
+      // timed in a finally like the reference's mainThreadDurationInThreadPool
+      // (multithread/index.ts:156-167): calls that throw are observed too
+      observe(this.metrics.lodestar_bls_thread_pool_main_thread_time_seconds, (now() - t0) / 1e3);
       this.prioBusy--;
     }
   }
@@ -355,7 +369,7 @@ class BlsGpuVerifier {
   verifySignatureSetsSync(sets) {
     if (this.closed) throw new QueueError();
     checkSets(sets);
-    const res = addon.verifySync(this.prio, encodeJobs([sets]));
+    const res = addon.verifySync(this.prio || this.ctx, encodeJobs([sets]));
     this.recordWork([{sets}], res);
     const o = jobOutcome(res.results[0]);
     if (!o.ok) throw o.error;
@@ -555,7 +569,7 @@ class BlsGpuVerifier {
     for (const job of this.jobs) job.reject(new QueueError());
     this.jobs = [];
     this.queuedSets = 0;
-    for (const c of this.ctxs.concat([this.prio])) addon.close(c); // each waits for its batch in flight (the context mutex)
+    for (const c of this.allContexts()) addon.close(c); // each waits for its batch in flight (the context mutex)
   }
 }
 

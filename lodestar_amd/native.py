@@ -50,7 +50,7 @@ EXPORTS = [
     "bgv_cfg_default", "bgv_close",
     "bgv_pubkeys_set", "bgv_pubkeys_count", "bgv_pubkeys_get", "bgv_pubkeys_validate", "bgv_verify", "bgv_last_stats",
     "bgv_partial", "bgv_partial_finish", "bgv_combine_final", "bgv_debug_stages", "bgv_gen_keys", "bgv_gen_sign", "bgv_bench_fpmul",
-    "bgv_bench_mad", "bgv_debug_fp_ops",
+    "bgv_bench_mad", "bgv_debug_fp_ops", "bgv_debug_g2_decode",
 ]
 FP_OPS_N = 13
 
@@ -227,6 +227,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
             "bgv_bench_fpmul": ([P, u32, u32, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
             "bgv_bench_mad": ([P, u32, u32, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
             "bgv_debug_fp_ops": ([P, P, u32, P], ctypes.c_int),
+            "bgv_debug_g2_decode": ([P, P, P, u32, P, P], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(lib, name)
@@ -422,6 +423,21 @@ class Device:
         out = np.zeros((n, FP_OPS_N, 12), np.uint32)
         self._check(self.lib.bgv_debug_fp_ops(self.h, ab.ctypes.data, n, out.ctypes.data))
         return out
+
+    def debug_g2_decode(self, sigs192: np.ndarray, sig_len: np.ndarray):
+        """Signature decode without the subgroup check (test only): sigs192 is
+        (n, 192) u8, sig_len (n,) u32; returns ((n, 192) u8 affine points as
+        x.c0 || x.c1 || y.c0 || y.c1 big-endian, (n,) i32 set codes)
+        (include/bgv.h bgv_debug_g2_decode)."""
+        sigs192 = np.ascontiguousarray(sigs192, dtype=np.uint8)
+        sig_len = np.ascontiguousarray(sig_len, dtype=np.uint32)
+        n = sig_len.shape[0]
+        assert sigs192.shape == (n, 192)
+        out = np.zeros((n, 192), np.uint8)
+        codes = np.zeros(n, np.int32)
+        self._check(self.lib.bgv_debug_g2_decode(self.h, sigs192.ctypes.data, sig_len.ctypes.data, n, out.ctypes.data,
+                                                 codes.ctypes.data))
+        return out, codes
 
     # ---------------------------------------------------------- microbench
     def bench_fpmul(self, lanes: int, iters: int) -> float:

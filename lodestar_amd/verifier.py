@@ -297,24 +297,34 @@ class BlsGpuVerifier:
 
     def __init__(self, devices=(0,), metrics: dict | None = None, scalar_seed: int | None = None,
                  max_sets_per_device_batch: int = MAX_SETS_PER_DEVICE_BATCH, shard_min_sets: int = SHARD_MIN_SETS,
-                 priority_cus: int = PRIORITY_CUS, bls_verify_all_multi_thread: bool = False):
-        # priority_cus CUs of the first device are kept for verifyOnMainThread
-        # (bgv_cfg.cu_split): its own context runs there, the first bulk
-        # context leaves them free; 0 shares every CU.
+                 priority_cus: int | None = None, bls_verify_all_multi_thread: bool = False):
+        # priority_cus CUs of the first device (a multiple of 8) are kept for
+        # verifyOnMainThread (bgv_cfg.cu_split): its own context runs there,
+        # the first bulk context leaves them free; 0 shares every CU.  Default:
+        # PRIORITY_CUS on a pool of two or more devices (sharded batches give
+        # device 0 a RESERVED_CAP-weighted shard), 0 on one device, whose bulk
+        # batches would otherwise run ~13-20% slower.
         # bls_verify_all_multi_thread (chain/options.ts:14, multithread/index.ts:124):
-        # verifyOnMainThread calls join the queue like any other, no CUs reserved
+        # verifyOnMainThread calls join the queue like any other, no CUs are
+        # reserved and no priority context is opened
+        devices = list(devices)
+        if priority_cus is None:
+            priority_cus = PRIORITY_CUS if len(devices) > 1 else 0
         if bls_verify_all_multi_thread:
             priority_cus = 0
         self.bls_verify_all_multi_thread = bls_verify_all_multi_thread
-        devices = list(devices)
+        self.priority_cus = priority_cus
         self.devices = [native.Device(d, cu_split=-priority_cus) if k == 0 and priority_cus > 0 else native.Device(d)
                         for k, d in enumerate(devices)]
-        self.prio = native.Device(devices[0], cu_split=priority_cus) if priority_cus > 0 else native.Device(devices[0])
+        if bls_verify_all_multi_thread:
+            self.prio = None
+        else:
+            self.prio = native.Device(devices[0], cu_split=priority_cus) if priority_cus > 0 else native.Device(devices[0])
         self.prio_reserved = priority_cus > 0  # device 0's bulk context runs at RESERVED_CAP (shard_jobs caps)
         self._prio_lock = threading.Lock()
         self._shard_min = shard_min_sets
         self._idle = [True] * len(self.devices)
-        self.table = PubkeyTable(self.devices + [self.prio])
+        self.table = PubkeyTable(self._contexts())
         self.metrics = metrics if metrics is not None else _new_metrics()
         self._rng = np.random.default_rng(scalar_seed) if scalar_seed is not None else None
         self._max_batch = max_sets_per_device_batch
@@ -370,7 +380,7 @@ class BlsGpuVerifier:
         self._jobs.clear()
         self._buffered.clear()
         self._exec.shutdown(wait=True)
-        for d in self.devices + [self.prio]:
+        for d in self._contexts():
             d.close()
 
     # -- synchronous helpers ------------------------------------------------
@@ -487,19 +497,25 @@ class BlsGpuVerifier:
         self.metrics["batch_sigs_success"] += int(st.batch_sigs_success)
         self.metrics["device_time_s"] += seconds
 
+    def _contexts(self) -> list:
+        return self.devices + ([self.prio] if self.prio is not None else [])
+
     def _run_priority(self, sets: list[ISignatureSet]):
         """verifyOnMainThread's device batch on the priority context"""
+        t0 = time.perf_counter()
         try:
             arrays = encode_jobs([sets], self._scalars(len(sets)))
             with self._prio_lock:
-                t0 = time.perf_counter()
+                t1 = time.perf_counter()
                 jr, _ = self.prio.verify(arrays, want_set_codes=False)
-                self._record(self.prio.last_stats, time.perf_counter() - t0)
-                # mainThreadDurationInThreadPool (multithread/index.ts:156-167)
-                self.metrics["main_thread_time_s"] += time.perf_counter() - t0
-                self.metrics["main_thread_calls"] += 1
+                self._record(self.prio.last_stats, time.perf_counter() - t1)
         except Exception as e:  # noqa: BLE001 -- a device error rejects the call
             return e
+        finally:
+            # mainThreadDurationInThreadPool (multithread/index.ts:156-167): timed
+            # in a finally, so calls that throw are observed too
+            self.metrics["main_thread_time_s"] += time.perf_counter() - t0
+            self.metrics["main_thread_calls"] += 1
         return self._verdict(int(jr[0]))
 
     def _run_device_batch(self, jobs: list[list[ISignatureSet]], devs: list[int] | None = None) -> list:

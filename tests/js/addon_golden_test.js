@@ -61,6 +61,7 @@ async function main() {
   interop.forEach((p, k) => pk48.set(hex(p), 48 * k));
 
   const verifier = new BlsGpuVerifier({device: 0});
+  assert.strictEqual(verifier.prioReserved, false, "one device: no CU reservation by default");
   verifier.syncPubkeys(0, pk48);
   const extra = new Uint8Array(96 * v.extra_table.length);
   v.extra_table.forEach((p, k) => extra.set(hex(p), 96 * k));
@@ -97,6 +98,10 @@ async function main() {
   assert.strictEqual(await verifier.verifySignatureSets(sets, {verifyOnMainThread: true}), true);
   assert.strictEqual(verifier.metrics.lodestar_bls_thread_pool_job_groups_started_total, groups0, "priority path skips the queue");
   assert.ok(verifier.metrics.lodestar_bls_thread_pool_main_thread_time_seconds.count >= 1, "main-thread duration series");
+  const mt0 = verifier.metrics.lodestar_bls_thread_pool_main_thread_time_seconds.count;
+  await assert.rejects(verifier.verifySignatureSets([{...sets[0], signature: new Uint8Array(32)}], {verifyOnMainThread: true}),
+    /BLST_INVALID_SIZE/);
+  assert.strictEqual(verifier.metrics.lodestar_bls_thread_pool_main_thread_time_seconds.count, mt0 + 1, "a throwing call is timed");
   assert.strictEqual(verifier.verifySignatureSetsSync(sets), true);  // BlsSingleThreadVerifier semantics
   const wrongMsg = sets.map((s, k) => (k === 1 ? {...s, signingRoot: hex(v.jobs[0].sets[0].msg).map((b) => b ^ 1)} : s));
   assert.strictEqual(await verifier.verifySignatureSets(wrongMsg), false);
@@ -194,6 +199,8 @@ async function main() {
   const allMt = new BlsGpuVerifier({device: 0, blsVerifyAllMultiThread: true});
   allMt.syncPubkeys(0, pk48);
   assert.strictEqual(allMt.prioReserved, false);
+  assert.strictEqual(allMt.prio, null, "no priority context is opened");
+  assert.strictEqual(allMt.verifySignatureSetsSync(sets), true, "the blocking path runs on the bulk context");
   const g0 = allMt.metrics.lodestar_bls_thread_pool_job_groups_started_total;
   assert.strictEqual(await allMt.verifySignatureSets(sets, {verifyOnMainThread: true}), true);
   assert.ok(allMt.metrics.lodestar_bls_thread_pool_job_groups_started_total > g0, "queued like any other call");
@@ -215,6 +222,7 @@ async function main() {
   // GPU 0 here) verify one batch split by job; partial Miller products, ONE
   // combined final exponentiation; a failing shard is localised per job
   const multi = new BlsGpuVerifier({devices: [0, 0], shardMinSets: 1});
+  assert.strictEqual(multi.prioReserved, true, "two devices: device 0 reserves CUs for verifyOnMainThread by default");
   multi.syncPubkeys(0, pk48);
   multi.pubkeysSet(v.extra_table_base, extra, 1);
   const jobSets = v.jobs.map((j) => j.sets);

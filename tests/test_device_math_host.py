@@ -92,6 +92,11 @@ def test_fp2_ops():
         o = H.buf(96)
         assert lib.hc_fp2_sqrt(H.fp2_b((a0, 0)), o) == 1
         assert B.f2_eq(B.f2_sqr(H.b_fp2(o.raw)), (a0, 0))
+        # the exact root: a0^((p+1)/4), or (-a0)^((p+1)/4) i for a non-residue
+        e = (B.P + 1) // 4
+        s = pow(a0, e, B.P)
+        want = (s, 0) if s * s % B.P == a0 % B.P else (0, pow(-a0 % B.P, e, B.P))
+        assert H.b_fp2(o.raw) == want
 
 
 def test_fp12_ops():

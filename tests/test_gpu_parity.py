@@ -211,10 +211,16 @@ def test_async_verifier_like_reference_e2e():
     async def run():
         pool = V.BlsGpuVerifier(devices=(0,))
         try:
+            assert not pool.prio_reserved  # one device: no CU reservation by default
             assert await pool.verify_signature_sets(sets)
             assert await pool.verify_signature_sets(sets, V.VerifySignatureOpts(batchable=True))
             assert await pool.verify_signature_sets(sets, V.VerifySignatureOpts(verifyOnMainThread=True))
             assert pool.metrics["main_thread_calls"] == 1  # mainThreadDurationInThreadPool
+            # a call that throws is timed too (the reference's finally, multithread/index.ts:156-167)
+            short = V.create_single_signature_set_from_components(sets[0].pubkey, sets[0].signingRoot, bytes(32))
+            with pytest.raises(V.BlsError, match="BLST_INVALID_SIZE"):
+                await pool.verify_signature_sets([short], V.VerifySignatureOpts(verifyOnMainThread=True))
+            assert pool.metrics["main_thread_calls"] == 2
             good = [pool.verify_signature_sets(sets, V.VerifySignatureOpts(batchable=True)) for _ in range(8)]
             bad_set = V.create_single_signature_set_from_components(sets[0].pubkey, sets[0].signingRoot, bytes(32))
             bad = pool.verify_signature_sets([bad_set], V.VerifySignatureOpts(batchable=True))
@@ -249,7 +255,7 @@ def test_async_verifier_like_reference_e2e():
             jobs0 = pool.metrics["jobs_started"]
             assert await pool.verify_signature_sets(sets, V.VerifySignatureOpts(verifyOnMainThread=True))
             assert pool.metrics["jobs_started"] > jobs0
-            assert not pool.prio_reserved
+            assert not pool.prio_reserved and pool.prio is None  # no priority context is opened
         finally:
             await pool.close()
 
