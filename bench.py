@@ -14,7 +14,9 @@ drawn (device ChaCha20 keyed by getrandom) and applied, one Miller loop per
 set, per-block products,
 and the final exponentiation (one for the segment; per-block ones only if
 it fails).  Inputs (indices, messages, signatures) are resident in HBM
-before the timed region.  Multi-GPU (weak scaling): every rank verifies its
+before the timed region.  --inflight D (default 3) batches are in flight per
+GPU, one context each, as a pool with D contexts per device runs them: the
+next batches' phase 1 fills the SIMDs a batch's Miller phase leaves idle.  Multi-GPU (weak scaling): every rank verifies its
 own 32-epoch segment (seeded per rank); each reduces its segment to one
 Fp12 Miller product, the 576-byte partials are all-gathered over RCCL and
 the node's ONE final exponentiation runs on their product.
@@ -46,6 +48,11 @@ ATT_PER_BLOCK = 95
 ATT_K = 128
 SYNC_K = 512
 SEED = 0x4C4F4445
+# batches in flight per GPU (one context each): the next batches' hash, pubkey
+# and decode kernels fill the SIMDs a batch's one-wave Miller phase leaves idle
+# (profiles/r06b_overlap_sizes.txt: C4 36.7 -> 34.2 / 33.1 ms per batch with
+# 2 / 3 in flight; C4/8 9.65 -> 8.35 / 7.59 ms with 3 / 4)
+INFLIGHT = 3
 
 
 def log(*a):
@@ -358,15 +365,22 @@ def host_resident_c4(d, arrays_host: dict, reps: int = 3):
                              + arrays_host["pk_offsets"].nbytes + arrays_host["job_offsets"].nbytes)}
 
 
-def shard_projection(d, torch, dev, arrays_host: dict, worlds=(2, 4, 8), reps: int = 5):
+def shard_projection(d, torch, dev, arrays_host: dict, ds=None, worlds=(2, 4, 8), reps: int = 5):
     """Strong sharding of ONE C4 segment measured on one GPU: each rank's
     shard (dist.shard_jobs) through bgv_partial, plus the node's combination of
     `world` partials (bgv_combine_final).  ms = median partial + combine; the
     RCCL all-gather of 576 B per rank is not included (latency-bound, ~tens of
-    us over xGMI).  projected_sets_per_s = 100,352 / ms."""
-    from lodestar_amd.dist import batch_job_work, select_jobs, shard_balance, shard_jobs
+    us over xGMI).  projected_sets_per_s = 100,352 / ms.  With `ds` (the
+    contexts of the batches in flight), ms_in_flight = the shard's time per
+    segment with len(ds) segments in flight (dist.run_in_flight: partials on
+    worker threads, combinations in order on this thread), the per-GPU pace of
+    a node verifying a stream of segments."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from lodestar_amd.dist import batch_job_work, run_in_flight, select_jobs, shard_balance, shard_jobs
     work = batch_job_work(arrays_host)
     out = {}
+    ex = ThreadPoolExecutor(max_workers=len(ds)) if ds and len(ds) > 1 else None
     for world in worlds:
         shards = shard_jobs(work, world)
         # the heaviest shard sets the node's time
@@ -383,9 +397,27 @@ def shard_projection(d, torch, dev, arrays_host: dict, worlds=(2, 4, 8), reps: i
             valid = d.combine_final([part] * world)
             t.append(time.perf_counter() - t1)
         ms = float(np.median(t)) * 1e3
-        out[f"c4_over_{world}"] = {"sets_per_rank": int(sub["n_sets"]), "ms": round(ms, 3),
-                                  "work_max_over_mean": round(shard_balance(work, shards), 4),
-                                  "projected_sets_per_s": round(arrays_host["n_sets"] / ms * 1e3, 1)}
+        e = {"sets_per_rank": int(sub["n_sets"]), "ms": round(ms, 3),
+             "work_max_over_mean": round(shard_balance(work, shards), 4),
+             "projected_sets_per_s": round(arrays_host["n_sets"] / ms * 1e3, 1)}
+        if ex is not None:
+            def submit(k):
+                return ex.submit(ds[k % len(ds)].partial, sub, on_device=True)
+
+            def finish(k, res):
+                return ds[k % len(ds)].combine_final([res[0]] * world) and res[3]
+
+            n = 4 * len(ds)
+            assert run_in_flight(submit, finish, len(ds), len(ds))
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            assert run_in_flight(submit, finish, n, len(ds))
+            mi = (time.perf_counter() - t1) / n * 1e3
+            e.update(ms_in_flight=round(mi, 3), inflight=len(ds),
+                     projected_sets_per_s_in_flight=round(arrays_host["n_sets"] / mi * 1e3, 1))
+        out[f"c4_over_{world}"] = e
+    if ex is not None:
+        ex.shutdown()
     return out
 
 
@@ -433,46 +465,60 @@ def reserved_device(d, gpu, torch, dev, darr, arrays_host: dict, reps: int = 5):
             "note": "pool default: reserved only with >= 2 devices (device 0); a one-device pool reserves nothing unless priorityCus asks"}
 
 
-def timed_steps(step, dist, coll_dev, torch, steps: int, warmup: int):
-    """W untimed + K timed steps between barriers; the max elapsed over ranks"""
-    for _ in range(warmup):
-        assert step(), "warm-up batch did not verify"
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ok = True
-    for _ in range(steps):
-        ok &= step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device=coll_dev if coll_dev is not None else "cpu", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    return elapsed, ok
+def one_in_flight(d, darr, torch, reps: int = 5):
+    """C4 verified back to back on one context: ms per batch (median) and the
+    per-stage HIP-event times of those batches (the isolated kernel durations)"""
+    from lodestar_amd import native
+    t, st = [], np.zeros(native.N_STAGES)
+    for k in range(reps + 1):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        jr, _ = d.verify(darr, on_device=True, want_set_codes=False)
+        assert (jr == 1).all()
+        if k:
+            t.append((time.perf_counter() - t1) * 1e3)
+            st += np.array(list(d.last_stats.stage_ms))
+    ms = float(np.median(t))
+    stage = {d.stage_name(i): float(st[i] / reps) for i in range(native.N_STAGES) if d.stage_name(i) != "unknown"}
+    return {"ms_p50": round(ms, 3), "sets_per_s": round(darr["n_sets"] / ms * 1e3, 1), "reps": reps}, stage
 
 
-def weak_leg(d, torch, dev, dist, coll_dev, rank, world, args):
+def weak_leg(ds, torch, dev, dist, coll_dev, rank, world, args):
     """N > 1 extra: every rank verifies its OWN whole segment (seeded per rank),
     one 576-B partial per rank all-gathered, ONE final exponentiation; the
-    node's sets/s over all ranks (weak scaling, not BASELINE configs[3])."""
-    from lodestar_amd.dist import verify_sharded
+    node's sets/s over all ranks (weak scaling, not BASELINE configs[3]),
+    len(ds) segments in flight per GPU like the main measurement."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from lodestar_amd.dist import combine_sharded, run_in_flight
     seg = build_segment(list(range(args.blocks)), seed=SEED + 7919 * (rank + 1))
     da = to_device(seg, torch, dev)
     sigs = torch.zeros((seg["n_sets"], 192), dtype=torch.uint8, device=dev)
-    d.gen_sign(da, sigs, on_device=True)
+    ds[0].gen_sign(da, sigs, on_device=True)
     da.update(sigs=sigs, sig_len=torch.full((seg["n_sets"],), 96, dtype=torch.int32, device=dev), scalars=None)
+    ex = ThreadPoolExecutor(max_workers=len(ds))
 
-    def step():
-        valid, jr = verify_sharded(d, da, dist, device=coll_dev, on_device=True)
+    def submit(k):
+        return ex.submit(ds[k % len(ds)].partial, da, on_device=True)
+
+    def finish(k, res):
+        valid, jr = combine_sharded(ds[k % len(ds)], res, dist, device=coll_dev)
         return valid and bool((jr == 1).all())
 
-    elapsed, ok = timed_steps(step, dist, coll_dev, torch, args.steps, max(args.warmup, 1))
+    assert run_in_flight(submit, finish, len(ds) + max(args.warmup, 1), len(ds)), "weak-leg warm-up did not verify"
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ok = run_in_flight(submit, finish, args.steps, len(ds))
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=coll_dev if coll_dev is not None else "cpu", dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    ex.shutdown()
     return {"sets_per_s": round(seg["n_sets"] * world * args.steps / elapsed, 1), "sets_per_rank": seg["n_sets"],
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "verified": ok,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "verified": ok, "inflight": len(ds),
             "note": "every rank its own 32-epoch segment; one partial per rank all-gathered, one final exponentiation"}
 
 
@@ -487,7 +533,10 @@ def main():
     ap.add_argument("--weak", action="store_true",
                     help="N > 1: every rank verifies its own segment (default: ONE segment split across the ranks, BASELINE configs[3])")
     ap.add_argument("--no-weak-leg", action="store_true", help="N > 1: skip the extra weak-scaling measurement")
+    ap.add_argument("--inflight", type=int, default=INFLIGHT,
+                    help="batches in flight per GPU: contexts on the GPU, one worker thread each (dist.run_in_flight)")
     args = ap.parse_args()
+    assert args.inflight >= 1
 
     import torch
 
@@ -520,6 +569,13 @@ def main():
     t0 = time.time()
     d.gen_keys(0, N_VALIDATORS, SEED)
     log(f"[bench] {N_VALIDATORS} keys generated in {time.time() - t0:.1f}s")
+    # the other contexts of the batches in flight: each holds its own table
+    # replica (as every context of the pools does) and its own streams
+    ds = [d]
+    for _ in range(args.inflight - 1):
+        x = native.Device(gpu)
+        x.gen_keys(0, N_VALIDATORS, SEED)
+        ds.append(x)
 
     seg = build_segment(list(range(args.blocks)), seed=SEED + (0 if shard else rank))
     jo = seg["job_offsets"]
@@ -536,34 +592,56 @@ def main():
     darr["scalars"] = None  # drawn by the library per call (device ChaCha20 keyed by getrandom)
     log(f"[bench] rank {rank}: {n_sets} sets signed in {time.time() - t0:.1f}s")
 
-    def step():
-        if world == 1:
-            jr, _ = d.verify(darr, on_device=True, want_set_codes=False)
-            return bool((jr == 1).all())
-        valid, local_jr = verify_sharded(d, darr, dist, device=coll_dev, on_device=True)
-        if shard:  # every rank ends with the whole segment's per-block verdicts
-            full = gather_job_results(local_jr, shards, seg["n_jobs"], dist, device=coll_dev)
-            return valid and bool((full == 1).all())
-        return valid and bool((local_jr == 1).all())
+    # a step = one batch: bgv_verify (N = 1) or this rank's shard through
+    # bgv_partial, then (in step order, on this thread) the all-gather of the
+    # partials, the combined final check and the per-block verdicts.  Steps
+    # go round-robin to the contexts, args.inflight of them outstanding; the
+    # batches read the same device-resident inputs (read-only) and draw their
+    # own scalars
+    from concurrent.futures import ThreadPoolExecutor
 
-    for _ in range(args.warmup):
-        assert step(), "warm-up batch did not verify"
+    from lodestar_amd.dist import combine_sharded, run_in_flight
+    ex = ThreadPoolExecutor(max_workers=args.inflight)
     stage_sum = np.zeros(native.N_STAGES)
-    step_ms = []
+    t_sub, lat = {}, []
+
+    def submit(k):
+        c = ds[k % len(ds)]
+        t_sub[k] = time.perf_counter()
+        if world == 1:
+            return ex.submit(c.verify, darr, on_device=True, want_set_codes=False)
+        return ex.submit(c.partial, darr, on_device=True)
+
+    def finish(k, res):
+        c = ds[k % len(ds)]
+        if world == 1:
+            ok = bool((res[0] == 1).all())
+        else:
+            valid, local_jr = combine_sharded(c, res, dist, device=coll_dev)
+            if shard:  # every rank ends with the whole segment's per-block verdicts
+                full = gather_job_results(local_jr, shards, seg["n_jobs"], dist, device=coll_dev)
+                ok = valid and bool((full == 1).all())
+            else:
+                ok = valid and bool((local_jr == 1).all())
+        lat.append((time.perf_counter() - t_sub.pop(k)) * 1e3)
+        stage_sum[:] += np.array(list(c.last_stats.stage_ms))
+        return ok
+
+    # every context verifies one batch first (its buffers sized), then W warm-up steps
+    assert run_in_flight(submit, finish, len(ds), len(ds)), "context priming batch did not verify"
+    assert run_in_flight(submit, finish, args.warmup, len(ds)), "warm-up batch did not verify"
+    stage_sum[:] = 0
+    lat.clear()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    all_ok = True
-    for _ in range(args.steps):
-        t1 = time.perf_counter()
-        all_ok &= step()
-        step_ms.append((time.perf_counter() - t1) * 1e3)
-        stage_sum += np.array(list(d.last_stats.stage_ms))
+    all_ok = run_in_flight(submit, finish, args.steps, len(ds))
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    step_ms = list(lat)
     if dist:
         t = torch.tensor([elapsed], device=coll_dev if coll_dev is not None else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -585,8 +663,13 @@ def main():
     stage_ms = {d.stage_name(i): float(stage_sum[i] / args.steps) for i in range(native.N_STAGES) if d.stage_name(i) != "unknown"}
 
     legs = {}
+    iso_stage_ms = None
+    if rank == 0 and world == 1:
+        # the same batch with ONE in flight (the r01-r05 step): its latency and
+        # the kernels' durations without other batches beside them
+        legs["one_in_flight"], iso_stage_ms = one_in_flight(d, darr, torch)
     if shard and not args.no_weak_leg:
-        legs["weak_scaling"] = weak_leg(d, torch, dev, dist, coll_dev, rank, world, args)
+        legs["weak_scaling"] = weak_leg(ds, torch, dev, dist, coll_dev, rank, world, args)
     if rank == 0 and world == 1 and not args.no_c2:
         legs.update(small_configs(d, torch, dev, arrays))
         host = dict(arrays)
@@ -597,7 +680,7 @@ def main():
         legs["c4_epoch_slice"] = epoch_slice(d, torch, dev, arrays, host["sigs"])
         legs["mixed_sizes"] = mixed_sizes(d, darr)
         if world == 1:
-            legs["strong_shard_projection"] = shard_projection(d, torch, dev, host)
+            legs["strong_shard_projection"] = shard_projection(d, torch, dev, host, ds)
             legs["reserved_device"] = reserved_device(d, gpu, torch, dev, darr, host)
 
     # roofline (INT32 VALU): algorithmic Fp-mul per set x sets / the stage's
@@ -639,6 +722,12 @@ def main():
                       "note": "96-B table row + 4-B index per pubkey reference; compute-bound (one G1 mixed addition per row)"}
         dom = max(stage_ms, key=stage_ms.get)
         e = per_stage.get(dom, {})
+        iso = None
+        if iso_stage_ms and dom in stage_counts and iso_stage_ms.get(dom, 0) > 0:
+            ach_i = stage_counts[dom] * n_sets / (iso_stage_ms[dom] * 1e-3) / 1e9
+            iso = {"kernel_ms": round(iso_stage_ms[dom], 3), "achieved": round(ach_i, 3), "frac": round(ach_i / peak_fpmul, 4),
+                   "stage_ms": {k: round(v, 3) for k, v in iso_stage_ms.items() if v > 0},
+                   "note": "the same kernel with ONE batch in flight (one_in_flight leg): no other batch shares the chip"}
         traffic, tsrc = pmc_traffic(dom)
         roof = {"bound": "valu-int32", "kernel": dom, "kernel_name": STAGE_KERNEL.get(dom),
                 "achieved": e.get("achieved_G_fpmul_per_s"), "peak": round(peak_fpmul, 3), "unit": "G Fp-mul/s",
@@ -648,7 +737,9 @@ def main():
                 "peak_def": "measured v_mad_u64_u32 lane-ops/s / 288 (12x32-bit CIOS product count)",
                 "mad_u64_lane_ops_per_s": mad_rate, "peak_fpmul28_G_per_s": round(mad_rate / 393 / 1e9, 3),
                 "fpmul_microbench_G_per_s": round(fpm_rate, 3),
-                "per_stage": per_stage, "pubkey_gather": gather,
+                "per_stage": per_stage, "pubkey_gather": gather, "isolated": iso,
+                "timing_note": ("kernel_ms: the stage's HIP-event time inside the timed region, where %d batches are in flight "
+                                "and share the chip" % args.inflight),
                 "miller_lines": ({"active": True, "kernel_name": "k_lines", "fpmul_per_set": counts["per_set_lines"]["miller_lines"],
                                   "note": "untimed step on the hash stream between hash_to_g2 and miller_loop"}
                                  if counts and lay["lines"] and "per_set_lines" in counts else {"active": False}),
@@ -662,6 +753,7 @@ def main():
         cpu = None if (args.no_cpu or world > 1) else cpu_baseline()
         par = (f"one segment sharded by job over {world} GPUs (shard_jobs), RCCL all-gather of Miller partials + per-job verdicts"
                if shard else f"one segment per GPU x{world}, RCCL all-gather of Miller partials")
+        par += f"; {args.inflight} batches in flight per GPU (contexts, dist.run_in_flight)"
         out = {
             "metric": "BLS signature sets verified/sec (node)",
             "value": round(value, 1),
@@ -677,8 +769,10 @@ def main():
             "data": "synthetic (device-generated keys/signatures, seeded)",
             "config": {"workload": "C4 range-sync segment: 32 epochs = %d blocks x 98 sets (95 att k=128, sync k=512, 2 singles), 1M-validator table in HBM" % args.blocks,
                        "sets": total_sets, "pubkey_refs": int(args.blocks * (ATT_PER_BLOCK * ATT_K + SYNC_K + 2)) * (1 if shard else world),
-                       "table_validators": N_VALIDATORS, "jobs": args.blocks * (1 if shard else world), "parallelism": par},
+                       "table_validators": N_VALIDATORS, "jobs": args.blocks * (1 if shard else world), "parallelism": par,
+                       "inflight": args.inflight},
             "c4_step_ms_p50": round(float(np.median(step_ms)), 3),
+            "c4_step_ms_note": "submit -> verdict of one batch with the others in flight; one_in_flight has the lone batch",
             **legs,
             "verified": all_ok,
             "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()},
@@ -686,7 +780,9 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    d.close()
+    ex.shutdown()
+    for c in ds:
+        c.close()
     if dist:
         dist.destroy_process_group()
 

@@ -126,6 +126,18 @@ def allgather_partials(partial: bytes, dist, device=None) -> list[bytes]:
     return [p.cpu().numpy().tobytes() for p in parts]
 
 
+def combine_sharded(dev, partial_result, dist, device=None):
+    """The exchange half of verify_sharded: this rank's bgv_partial result
+    (as dev.partial returns it) -> all-gather -> combined final check on
+    `dev` (the context that made the partial), and the per-shard
+    localisation when it fails.  Returns (node_batch_valid, local_job_results)."""
+    part, _, jobs, _ = partial_result
+    parts = allgather_partials(part, dist, device)
+    if dev.combine_final(parts):
+        return True, np.asarray(jobs, np.int32)
+    return False, np.asarray(dev.partial_finish(), np.int32)
+
+
 def verify_sharded(dev, arrays: dict, dist, device=None, on_device: bool = False):
     """This rank's shard -> partial -> all-gather -> combined final check, and
     the per-shard localisation when it fails.
@@ -134,11 +146,35 @@ def verify_sharded(dev, arrays: dict, dist, device=None, on_device: bool = False
     this shard's job j as bgv_verify reports it (1 valid, 0 invalid, -code
     rejected).  Every rank takes the same branch (the combined verdict is
     computed from the same all-gathered partials)."""
-    part, _, jobs, _ = dev.partial(arrays, on_device=on_device)
-    parts = allgather_partials(part, dist, device)
-    if dev.combine_final(parts):
-        return True, np.asarray(jobs, np.int32)
-    return False, np.asarray(dev.partial_finish(), np.int32)
+    return combine_sharded(dev, dev.partial(arrays, on_device=on_device), dist, device)
+
+
+def run_in_flight(submit, finish, steps: int, depth: int) -> bool:
+    """Several batches in flight on one GPU.  Step k's device work goes to
+    context k % depth through submit(k) -> concurrent.futures.Future (a worker
+    thread: the library's calls release the GIL, and every context has its
+    own streams), while the calling thread finishes the steps IN ORDER with
+    finish(k, result) -> bool: the collectives of a sharded step (so every
+    rank issues its all-gathers in the same order from one thread) and the
+    verdict checks.  At most `depth` steps are outstanding, so context
+    k % depth has been finished when step k is submitted to it.  The next
+    batch's hash, pubkey and decode kernels then fill the SIMDs that a
+    batch's Miller phase leaves idle (C4: 36.7 -> 33.1 ms per batch with
+    three in flight, profiles/r06b_overlap_sizes.txt).  Returns the AND of
+    the finishes."""
+    from collections import deque
+
+    pending: deque = deque()
+    ok = True
+    for k in range(steps):
+        if len(pending) == depth:
+            j, fut = pending.popleft()
+            ok &= bool(finish(j, fut.result()))
+        pending.append((k, submit(k)))
+    while pending:
+        j, fut = pending.popleft()
+        ok &= bool(finish(j, fut.result()))
+    return ok
 
 
 def gather_job_results(local: np.ndarray, shards: list[list[int]], n_jobs: int, dist, device=None) -> np.ndarray:

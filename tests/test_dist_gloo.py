@@ -109,6 +109,109 @@ def test_sharded_verdicts_gloo_world2():
     assert max(loads) - min(loads) <= max(w)  # whole jobs: at most one job apart
 
 
+class FakeStepDevice(FakeShardDevice):
+    """one context of several in flight: the batch carries its own truth"""
+
+    def __init__(self):
+        super().__init__([])
+
+    def partial(self, arrays, on_device=False):
+        self.truth = np.asarray(arrays["truth"], np.int32)
+        return super().partial(arrays, on_device)
+
+
+STEP_TRUTHS = [
+    [1] * 10,
+    [1, 1, 1, 1, 1, 1, 0, 1, 1, 1],
+    [1, -3, 1, 1, 1, 1, 1, 1, 0, 1],
+    [1] * 10,
+    [1, 1, 1, 1, -8, 1, 1, 1, 1, 1],
+    [0] + [1] * 9,
+    [1] * 10,
+]
+
+
+def _worker_in_flight(rank, world, port, q, depth):
+    """dist.run_in_flight: `depth` contexts per rank, the device work on worker
+    threads, the exchanges of every step on the main thread in step order"""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import torch.distributed as dist
+    from lodestar_amd.dist import combine_sharded, gather_job_results, job_work, run_in_flight, shard_jobs
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    shards = shard_jobs(job_work(JOB_SETS, JOB_REFS), world)
+    devs = [FakeStepDevice() for _ in range(depth)]
+    got, submitted, finished = {}, [], []
+    ex = ThreadPoolExecutor(max_workers=depth)
+
+    def submit(k):
+        submitted.append(k)
+        assert k - len(finished) <= depth  # never more than `depth` outstanding
+        return ex.submit(devs[k % depth].partial, {"jobs": shards[rank], "truth": STEP_TRUTHS[k]})
+
+    def finish(k, res):
+        finished.append(k)
+        valid, local = combine_sharded(devs[k % depth], res, dist)
+        got[k] = (valid, gather_job_results(local, shards, 10, dist).tolist())
+        return valid
+
+    ok = run_in_flight(submit, finish, len(STEP_TRUTHS), depth)
+    ex.shutdown()
+    q.put((rank, {"ok": ok, "got": got, "order": finished, "submitted": submitted}))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("depth", [1, 3])
+def test_in_flight_sharded_steps_gloo_world2(depth):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_in_flight, args=(r, world, port, q, depth)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=150) for _ in range(world))
+    for p in ps:
+        p.join(timeout=30)
+    for rank in range(world):
+        o = res[rank]
+        assert o["order"] == list(range(len(STEP_TRUTHS)))  # finished in step order
+        assert o["submitted"] == list(range(len(STEP_TRUTHS)))
+        for k, t in enumerate(STEP_TRUTHS):
+            valid, full = o["got"][k]
+            assert full == t, (rank, k)
+            assert valid == all(x == 1 or x < 0 for x in t)
+        assert o["ok"] == all(all(x == 1 or x < 0 for x in t) for t in STEP_TRUTHS)
+
+
+def test_run_in_flight_order_and_depth():
+    """single process: at most `depth` outstanding, finishes in order, AND of the finishes"""
+    from concurrent.futures import Future
+
+    from lodestar_amd.dist import run_in_flight
+    live, peak, done = set(), [0], []
+
+    def submit(k):
+        live.add(k)
+        peak[0] = max(peak[0], len(live))
+        f = Future()
+        f.set_result(k * k)
+        return f
+
+    def finish(k, r):
+        live.discard(k)
+        done.append((k, r))
+        return k != 4
+
+    assert run_in_flight(submit, finish, 9, 3) is False
+    assert done == [(k, k * k) for k in range(9)] and peak[0] == 3
+    done.clear()
+    assert run_in_flight(submit, lambda k, r: done.append(k) or True, 0, 2) is True and done == []
+
+
 def test_select_jobs_rebases_offsets():
     from lodestar_amd.dist import select_jobs
     arrays = {"n_sets": 5, "n_jobs": 3, "job_offsets": np.array([0, 2, 3, 5], np.uint32),
