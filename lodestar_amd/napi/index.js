@@ -90,6 +90,11 @@ const RESERVED_CAP = require("./reserved_cap.json").RESERVED_CAP; // dist.py RES
 // exponentiation); smaller batches run whole on one device while the other
 // devices take the next batch (lodestar_amd/verifier.py SHARD_MIN_SETS)
 const SHARD_MIN_SETS = 4096;
+// device batches in flight per GPU, one context each: the next batches' hash,
+// pubkey and decode kernels fill the SIMDs that a batch's one-wave Miller
+// phase leaves idle (C4 36.7 -> 33.1 ms per batch with 3, C4/8 shards
+// 9.65 -> 8.35 ms; profiles/r06b_overlap_sizes.txt, DESIGN.md §5)
+const CONTEXTS_PER_DEVICE = 3;
 // non-batchable jobs start once a macro task passes without a new job
 // (bounded), so the per-block calls of a range-sync segment
 // (verifyBlocksSignatures.ts:30-47, sleep(0) every 8 blocks) coalesce
@@ -257,9 +262,13 @@ class BlsGpuVerifier {
   // blsVerifyAllMultiThread (chain/options.ts:14, multithread/index.ts:124): verifyOnMainThread
   // calls join the pool's queue like any other; no CUs are then reserved and
   // no priority context is opened
+  // contextsPerDevice: device batches in flight per GPU (one context each,
+  // each with its own table replica); a batch large enough to shard is split
+  // over one idle context per device
   constructor({device = 0, devices = null, maxSetsPerDeviceBatch = MAX_SETS_PER_DEVICE_BATCH, shardMinSets = SHARD_MIN_SETS,
-    priorityCus = null, blsVerifyAllMultiThread = false} = {}) {
+    priorityCus = null, blsVerifyAllMultiThread = false, contextsPerDevice = CONTEXTS_PER_DEVICE} = {}) {
     const ids = devices && devices.length ? devices : [device];
+    if (!(contextsPerDevice >= 1)) throw new Error(`contextsPerDevice ${contextsPerDevice}`);
     if (priorityCus === null || priorityCus === undefined) priorityCus = ids.length > 1 ? PRIORITY_CUS : 0;
     if (blsVerifyAllMultiThread) priorityCus = 0;
     this.blsVerifyAllMultiThread = blsVerifyAllMultiThread;
@@ -270,12 +279,25 @@ class BlsGpuVerifier {
     // 16 this module assigns when it was unset only counts if the pool had
     // not started yet, which the module cannot tell, so it assumes libuv's 4
     const pool = Number(UV_POOL_PRESET) || 4;
-    if (ids.length + 2 > pool) {
+    const nCtx = ids.length * contextsPerDevice;
+    if (nCtx + 2 > pool) {
       const was = UV_POOL_PRESET ? `UV_THREADPOOL_SIZE=${pool}` : "UV_THREADPOOL_SIZE unset at start (libuv default 4)";
-      console.warn(`BlsGpuVerifier: ${ids.length} devices with ${was}: device batches may ` +
-        "serialise and starve other pool work; start Node with UV_THREADPOOL_SIZE >= devices + 2");
+      console.warn(`BlsGpuVerifier: ${nCtx} device contexts with ${was}: device batches may ` +
+        "serialise and starve other pool work; start Node with UV_THREADPOOL_SIZE >= contexts + 2");
     }
-    this.ctxs = ids.map((d, k) => addon.open(d, k === 0 && priorityCus > 0 ? -priorityCus : 0));
+    // context k runs on device entry ctxDev[k]; every bulk context of the first
+    // device leaves the reserved CUs free (one unmasked context would put bulk
+    // waves on them)
+    this.ctxDev = [];
+    this.ctxs = [];
+    ids.forEach((d, i) => {
+      for (let c = 0; c < contextsPerDevice; c++) {
+        this.ctxs.push(addon.open(d, i === 0 && priorityCus > 0 ? -priorityCus : 0));
+        this.ctxDev.push(i);
+      }
+    });
+    this.nDevices = ids.length;
+    this.contextsPerDevice = contextsPerDevice;
     this.ctx = this.ctxs[0];
     // verifyOnMainThread's own context (with its own table replica and mutex):
     // it never waits for a bulk batch's context lock or, with priorityCus, its
@@ -285,7 +307,7 @@ class BlsGpuVerifier {
     this.prioReserved = priorityCus > 0;
     this.priorityCus = priorityCus;
     this.prioBusy = 0;
-    this.idle = ids.map(() => true);
+    this.idle = this.ctxs.map(() => true);
     this.maxSetsPerDeviceBatch = maxSetsPerDeviceBatch;
     this.shardMinSets = shardMinSets;
     this.jobs = [];
@@ -438,13 +460,29 @@ class BlsGpuVerifier {
     return jobs;
   }
 
-  // multithread/index.ts:297-391: every idle device takes a device batch; a
-  // batch of >= shardMinSets sets is split over all idle devices instead
+  // idle contexts: the first idle one of each device (spread, for sharding)
+  // and the idle one on the least busy device (for a whole batch)
+  idleContexts() {
+    const busyOn = new Array(this.nDevices).fill(0);
+    this.idle.forEach((f, k) => { if (!f) busyOn[this.ctxDev[k]]++; });
+    const spread = [];
+    const seen = new Set();
+    let best = -1;
+    this.idle.forEach((f, k) => {
+      if (!f) return;
+      const dv = this.ctxDev[k];
+      if (!seen.has(dv)) { seen.add(dv); spread.push(k); }
+      if (best < 0 || busyOn[dv] < busyOn[this.ctxDev[best]]) best = k;
+    });
+    return {spread, best};
+  }
+
+  // multithread/index.ts:297-391: every idle context takes a device batch; a
+  // batch of >= shardMinSets sets is split over one idle context per device
   runJob() {
     this.runScheduled = false;
     while (!this.closed && this.jobs.length > 0) {
-      const idle = [];
-      this.idle.forEach((f, k) => f && idle.push(k));
+      const {spread: idle, best} = this.idleContexts();
       if (idle.length === 0) return; // a finishing batch reschedules
       if (this.pushSeq !== this.seenSeq && this.quietWaits < MAX_QUIET_WAITS) {
         // jobs arrived since the last look: wait one more macro task
@@ -458,7 +496,7 @@ class BlsGpuVerifier {
       const jobs = this.prepareWork();
       let n = 0;
       for (const j of jobs) n += j.sets.length;
-      const devs = idle.length > 1 && jobs.length > 1 && n >= this.shardMinSets ? idle : [idle[0]];
+      const devs = idle.length > 1 && jobs.length > 1 && n >= this.shardMinSets ? idle : [best];
       for (const k of devs) this.idle[k] = false;
       this.runDeviceBatch(jobs, devs);
     }
@@ -466,6 +504,7 @@ class BlsGpuVerifier {
 
   async runDeviceBatch(jobs, devs) {
     this.busy++;
+    this.peakBusy = Math.max(this.peakBusy || 0, this.busy); // device batches in flight at once (test hook)
     const m = this.metrics;
     try {
       const now = Date.now();
@@ -502,7 +541,7 @@ class BlsGpuVerifier {
   async verifySharded(jobSets, devs) {
     // the first device's bulk context leaves CUs to the priority context and
     // runs at RESERVED_CAP of the others' pace (dist.py)
-    const caps = devs.map((d) => (d === 0 && this.prioReserved ? RESERVED_CAP : 1));
+    const caps = devs.map((k) => (this.ctxDev[k] === 0 && this.prioReserved ? RESERVED_CAP : 1));
     const shards = shardJobs(jobSets.map(jobWork), devs.length, caps);
     const live = [];
     shards.forEach((ids, r) => ids.length && live.push({ctx: this.ctxs[devs[r]], ids}));
@@ -618,5 +657,5 @@ class BlsGpuSingleThreadVerifier {
 
 module.exports = {
   addon, BlsGpuVerifier, BlsGpuSingleThreadVerifier, QueueError, sourceHash, checkBuildId, chunkifyMaximizeChunkSize, encodeJobs, checkSets, shardJobs, jobWork,
-  MAX_BUFFERED_SIGS, MAX_BUFFER_WAIT_MS, MAX_JOBS_CAN_ACCEPT_WORK, SHARD_MIN_SETS, PRIORITY_CUS, RESERVED_CAP,
+  MAX_BUFFERED_SIGS, MAX_BUFFER_WAIT_MS, MAX_JOBS_CAN_ACCEPT_WORK, SHARD_MIN_SETS, PRIORITY_CUS, RESERVED_CAP, CONTEXTS_PER_DEVICE,
 };

@@ -51,6 +51,10 @@ MAX_BUFFERED_SIGS = 32            # multithread/index.ts:48
 MAX_BUFFER_WAIT_MS = 100          # multithread/index.ts:57
 MAX_JOBS_CAN_ACCEPT_WORK = 512    # multithread/index.ts:62
 PRIORITY_CUS = 32  # CUs of the first device kept for verifyOnMainThread (bgv_cfg.cu_split; one per SE)
+# device batches in flight per GPU, one context each (napi/index.js
+# CONTEXTS_PER_DEVICE): the next batches' phase 1 fills the SIMDs a batch's
+# Miller phase leaves idle (profiles/r06b_overlap_sizes.txt)
+CONTEXTS_PER_DEVICE = 3
 MAX_SETS_PER_DEVICE_BATCH = 1 << 17
 # a device batch of at least this many sets (and >= 2 jobs) is split by job
 # over the idle devices: each returns a partial Miller product and ONE final
@@ -297,7 +301,8 @@ class BlsGpuVerifier:
 
     def __init__(self, devices=(0,), metrics: dict | None = None, scalar_seed: int | None = None,
                  max_sets_per_device_batch: int = MAX_SETS_PER_DEVICE_BATCH, shard_min_sets: int = SHARD_MIN_SETS,
-                 priority_cus: int | None = None, bls_verify_all_multi_thread: bool = False):
+                 priority_cus: int | None = None, bls_verify_all_multi_thread: bool = False,
+                 contexts_per_device: int = CONTEXTS_PER_DEVICE):
         # priority_cus CUs of the first device (a multiple of 8) are kept for
         # verifyOnMainThread (bgv_cfg.cu_split): its own context runs there,
         # the first bulk context leaves them free; 0 shares every CU.  Default:
@@ -314,8 +319,16 @@ class BlsGpuVerifier:
             priority_cus = 0
         self.bls_verify_all_multi_thread = bls_verify_all_multi_thread
         self.priority_cus = priority_cus
-        self.devices = [native.Device(d, cu_split=-priority_cus) if k == 0 and priority_cus > 0 else native.Device(d)
-                        for k, d in enumerate(devices)]
+        # contexts_per_device device batches in flight per GPU (one context
+        # each, own table replica); every bulk context of the first device
+        # leaves the reserved CUs free.  Context k runs on device entry _ctx_dev[k]
+        if contexts_per_device < 1:
+            raise ValueError(f"contexts_per_device {contexts_per_device}")
+        self.contexts_per_device = contexts_per_device
+        self.n_devices = len(devices)
+        self._ctx_dev = [i for i in range(len(devices)) for _ in range(contexts_per_device)]
+        self.devices = [native.Device(devices[i], cu_split=-priority_cus) if i == 0 and priority_cus > 0
+                        else native.Device(devices[i]) for i in self._ctx_dev]
         if bls_verify_all_multi_thread:
             self.prio = None
         else:
@@ -450,11 +463,12 @@ class BlsGpuVerifier:
                 j = self._jobs.pop(0)
                 take.append(j)
                 n += len(j.sets)
-            idle = [d for d, f in enumerate(self._idle) if f]
-            devs = idle if (len(idle) > 1 and len(take) > 1 and n >= self._shard_min) else idle[:1]
+            idle = self._spread_contexts(idle_only=True)
+            devs = idle if (len(idle) > 1 and len(take) > 1 and n >= self._shard_min) else [self._best_idle_context()]
             for d in devs:
                 self._idle[d] = False
             self._busy += 1
+            self.peak_busy = max(getattr(self, "peak_busy", 0), self._busy)  # batches in flight at once (test hook)
             asyncio.ensure_future(self._run(take, devs))
 
     async def _run(self, jobs: list[_Job], devs: list[int]):
@@ -500,6 +514,23 @@ class BlsGpuVerifier:
     def _contexts(self) -> list:
         return self.devices + ([self.prio] if self.prio is not None else [])
 
+    def _spread_contexts(self, idle_only: bool = False) -> list[int]:
+        """the first (idle) context of each device: where a sharded batch goes"""
+        out, seen = [], set()
+        for k, dv in enumerate(self._ctx_dev):
+            if dv not in seen and (not idle_only or self._idle[k]):
+                seen.add(dv)
+                out.append(k)
+        return out
+
+    def _best_idle_context(self) -> int:
+        """an idle context on the device with the fewest batches in flight"""
+        busy = [0] * self.n_devices
+        for k, f in enumerate(self._idle):
+            if not f:
+                busy[self._ctx_dev[k]] += 1
+        return min((k for k, f in enumerate(self._idle) if f), key=lambda k: (busy[self._ctx_dev[k]], k))
+
     def _run_priority(self, sets: list[ISignatureSet]):
         """verifyOnMainThread's device batch on the priority context"""
         t0 = time.perf_counter()
@@ -528,10 +559,10 @@ class BlsGpuVerifier:
         own device."""
         if not jobs:
             return []
-        devs = list(range(len(self.devices))) if devs is None else list(devs)
+        devs = self._spread_contexts() if devs is None else list(devs)
         if len(devs) > 1:
             refs = [sum(1 if s.type == SignatureSetType.single else len(s.pubkeys) for s in j) for j in jobs]
-            caps = [RESERVED_CAP if d == 0 and self.prio_reserved else 1.0 for d in devs]
+            caps = [RESERVED_CAP if self._ctx_dev[d] == 0 and self.prio_reserved else 1.0 for d in devs]
             shards = shard_jobs(job_work([len(j) for j in jobs], refs), len(devs), caps)
         else:
             shards = [list(range(len(jobs)))]

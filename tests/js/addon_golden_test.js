@@ -194,6 +194,22 @@ async function main() {
   assert.strictEqual(small.canAcceptWork(), true);
   await small.close();
 
+  // 5a. device batches in flight: calls that arrive while a batch runs go to
+  // another context of the same GPU at once (contextsPerDevice, default 3)
+  const inf = new BlsGpuVerifier({device: 0});
+  assert.strictEqual(inf.ctxs.length, 3);
+  inf.syncPubkeys(0, pk48);
+  const fa = Promise.all(Array.from({length: 16}, () => inf.verifySignatureSets(sets)));
+  await sleep0();
+  await sleep0();
+  const fb = inf.verifySignatureSets(wrongMsg);
+  await sleep0();
+  await sleep0();
+  const fc = inf.verifySignatureSets(sets);
+  assert.deepStrictEqual(await Promise.all([fa, fb, fc]), [new Array(16).fill(true), false, true]);
+  assert.ok(inf.peakBusy >= 2, `batches in flight at once: ${inf.peakBusy}`);
+  await inf.close();
+
   // 5b. blsVerifyAllMultiThread (chain/options.ts:14): verifyOnMainThread calls
   // join the queue like any other, and no CUs are reserved
   const allMt = new BlsGpuVerifier({device: 0, blsVerifyAllMultiThread: true});
@@ -226,13 +242,17 @@ async function main() {
   multi.syncPubkeys(0, pk48);
   multi.pubkeysSet(v.extra_table_base, extra, 1);
   const jobSets = v.jobs.map((j) => j.sets);
-  const mres = await multi.verifySharded(goldenJobSets(v), [0, 1]);
+  // one context of each device entry (contexts 0 .. contextsPerDevice - 1 are the first device's)
+  assert.strictEqual(multi.ctxs.length, 2 * multi.contextsPerDevice);
+  const two = [0, multi.contextsPerDevice];
+  assert.deepStrictEqual(multi.idleContexts().spread, two);
+  const mres = await multi.verifySharded(goldenJobSets(v), two);
   assert.strictEqual(mres.shards, 2);
   assert.deepStrictEqual(Array.from(mres.results), expected, "sharded golden batch (faulted shards) vs golden");
   assert.deepStrictEqual(Array.from(mres.results), Array.from(got.results), "sharded == bgv_verify");
   assert.strictEqual(mres.batchRetries, 1);
   const clean = v.jobs.map((j, k) => k).filter((k) => v.jobs[k].expected === 1);
-  const cres = await multi.verifySharded(clean.map((k) => goldenJobSets(v)[k]), [0, 1]);
+  const cres = await multi.verifySharded(clean.map((k) => goldenJobSets(v)[k]), two);
   assert.deepStrictEqual(Array.from(cres.results), clean.map(() => 1), "sharded clean batch");
   assert.strictEqual(cres.batchRetries, 0);
   // and through the pool: 32 block-sized calls split over both contexts

@@ -127,7 +127,8 @@ def test_c2_gossip_batch(big):
 
     pool = V.BlsGpuVerifier(devices=(0,))
     try:
-        pool.devices[0].gen_keys(0, N_TABLE, SEED)
+        for c in pool._contexts():  # every context's table replica (batches in flight go to any of them)
+            c.gen_keys(0, N_TABLE, SEED)
         assert asyncio.run(run(pool)) == [True, False]
         assert pool.metrics["aggregated_pubkeys_total"] == 2 * n2 * k2
     finally:
@@ -143,7 +144,8 @@ def test_c3_blocks_first_invalid(coalesce, att_k):
     pool = V.BlsGpuVerifier(devices=(0,))
     try:
         d = pool.devices[0]
-        d.gen_keys(0, N_TABLE, SEED)
+        for c in pool._contexts():  # every context's table replica
+            c.gen_keys(0, N_TABLE, SEED)
         blocks, arrays = [], []
         for b in range(3):
             a = bench.build_segment([b], seed=SEED + 2000, att_per_block=128, att_k=att_k)
@@ -223,3 +225,32 @@ def test_c5_half_segment_deferred_subgroup_checks(big):
     jo = a["job_offsets"]
     mixed = [j for j in range(512) if 3 in sc[jo[j]:jo[j + 1]].tolist() and 1 in sc[jo[j]:jo[j + 1]].tolist()]
     assert any(expect[j] == -3 for j in mixed) and any(expect[j] == -1 for j in mixed)
+
+
+def test_pool_batches_in_flight_on_one_device():
+    """contexts_per_device (default 3): block calls that arrive while a device
+    batch runs go to another context of the same GPU at once, and every
+    verdict is that block's (one wrong-message block among eight)"""
+    from lodestar_amd import verifier as V
+    pool = V.BlsGpuVerifier(devices=(0,))
+    try:
+        assert len(pool.devices) == V.CONTEXTS_PER_DEVICE
+        for c in pool._contexts():
+            c.gen_keys(0, N_TABLE, SEED)
+        a = _sign(pool.devices[0], bench.build_segment(list(range(8)), seed=SEED + 6000))
+        blocks = G.sets_from_arrays(a)
+        bad = list(blocks[5])
+        bad[7] = V.create_aggregate_signature_set_from_components(bad[7].pubkeys, bad[8].signingRoot, bad[7].signature)
+        blocks[5] = bad
+
+        async def run():
+            futs = []
+            for k, b in enumerate(blocks):
+                futs.append(asyncio.ensure_future(pool.verify_signature_sets(b)))
+                await asyncio.sleep(0.002)  # the next block arrives while this one runs
+            return await asyncio.gather(*futs)
+
+        assert asyncio.run(run()) == [k != 5 for k in range(8)]
+        assert pool.peak_busy >= 2, pool.peak_busy
+    finally:
+        asyncio.run(pool.close())
