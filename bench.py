@@ -535,8 +535,11 @@ def main():
     ap.add_argument("--no-weak-leg", action="store_true", help="N > 1: skip the extra weak-scaling measurement")
     ap.add_argument("--inflight", type=int, default=INFLIGHT,
                     help="batches in flight per GPU: contexts on the GPU, one worker thread each (dist.run_in_flight)")
+    ap.add_argument("--cfg", action="append", default=[], metavar="KEY=VAL",
+                    help="bgv_cfg override for every context (A/B runs only, e.g. pairs=4)")
     args = ap.parse_args()
     assert args.inflight >= 1
+    cfg = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in args.cfg}
 
     import torch
 
@@ -565,7 +568,7 @@ def main():
     # add ~5 us of queue time per event on the critical path (C4/8 shard 9.65 ->
     # 9.75 ms, profiles/r04g_sweep_timed.txt), so the timed steps of N > 1 run
     # without them and one extra step on a timed context gives the breakdown
-    d = native.Device(gpu)
+    d = native.Device(gpu, **cfg)
     t0 = time.time()
     d.gen_keys(0, N_VALIDATORS, SEED)
     log(f"[bench] {N_VALIDATORS} keys generated in {time.time() - t0:.1f}s")
@@ -573,7 +576,7 @@ def main():
     # replica (as every context of the pools does) and its own streams
     ds = [d]
     for _ in range(args.inflight - 1):
-        x = native.Device(gpu)
+        x = native.Device(gpu, **cfg)
         x.gen_keys(0, N_VALIDATORS, SEED)
         ds.append(x)
 
@@ -699,6 +702,9 @@ def main():
         lay = timed_layout
         if counts and lay["lines"] and "per_set_lines" in counts:
             stage_counts["miller_loop"] = counts["per_set_lines"]["miller_loop"]
+        if counts and lay["lines"] and lay["pairs_per_item"] == 4 and "per_set_lines4" in counts:
+            stage_counts["miller_loop"] = counts["per_set_lines4"]["miller_loop"]
+            stage_counts["miller_product_tree"] = counts["per_set_lines4"]["miller_product_tree"]
         share = (n_sets - min(lay["defer_from"], n_sets)) / max(n_sets, 1)
         check_c = None
         if counts and "g2_decompress_only" in counts:
@@ -720,6 +726,11 @@ def main():
             gather = {"kernel": "k_pk_chunk", "algorithmic_bytes": pk_refs * (96 + 4), "ms": round(stage_ms["pk_gather"], 3),
                       "GB_per_s": round(gb, 1), "hbm_peak_GB_per_s": 8000, "frac_hbm": round(gb / 8000, 4),
                       "note": "96-B table row + 4-B index per pubkey reference; compute-bound (one G1 mixed addition per row)"}
+        step_total = None
+        if counts:
+            step_total = counts["per_set_total"]
+            if lay["lines"] and lay["pairs_per_item"] == 4 and "per_set_total_lines4" in counts:
+                step_total = counts["per_set_total_lines4"]
         dom = max(stage_ms, key=stage_ms.get)
         e = per_stage.get(dom, {})
         iso = None
@@ -747,7 +758,8 @@ def main():
                 "deferred_subgroup_checks": {"share_of_sets": share, "kernel_name": "k_sig_split",
                                              "fpmul_per_set": round(share * check_c, 1) if check_c is not None else None,
                                              "note": "untimed: beside the Miller loops, before the fold"},
-                "step_fpmul_G_per_s": round(counts["per_set_total"] * n_sets / (ms_per_step * 1e-3) / 1e9, 3) if counts else None}
+                "step_fpmul_per_set": step_total,
+                "step_fpmul_G_per_s": round(step_total * n_sets / (ms_per_step * 1e-3) / 1e9, 3) if counts else None}
 
     if rank == 0:
         cpu = None if (args.no_cpu or world > 1) else cpu_baseline()
@@ -770,7 +782,7 @@ def main():
             "config": {"workload": "C4 range-sync segment: 32 epochs = %d blocks x 98 sets (95 att k=128, sync k=512, 2 singles), 1M-validator table in HBM" % args.blocks,
                        "sets": total_sets, "pubkey_refs": int(args.blocks * (ATT_PER_BLOCK * ATT_K + SYNC_K + 2)) * (1 if shard else world),
                        "table_validators": N_VALIDATORS, "jobs": args.blocks * (1 if shard else world), "parallelism": par,
-                       "inflight": args.inflight},
+                       "inflight": args.inflight, **({"cfg_overrides": cfg} if cfg else {})},
             "c4_step_ms_p50": round(float(np.median(step_ms)), 3),
             "c4_step_ms_note": "submit -> verdict of one batch with the others in flight; one_in_flight has the lone batch",
             **legs,

@@ -165,7 +165,7 @@ typedef struct bgv_cfg {
   int32_t job_lanes;    /* 0 auto (36); 6 / 18 / 36: lanes of the per-job (-G1, S_job) pairs */
   int32_t msm;          /* -1 auto; 0 per-set [r_i] sigma_i + tree; 1 per-job bucket MSM (one workgroup per job); 2 the (job, window)-lane MSM;
                            3 one-lane per-set [r_i] sigma_i + tree, subgroup checks deferred; 4 the (job, window, digit)-lane MSM */
-  int32_t pairs;        /* 0 auto; 1 / 2 pairs per one-lane Miller work item */
+  int32_t pairs;        /* 0 auto; 1 / 2 / 4 pairs per one-lane Miller work item (4: over precomputed lines only, else 2) */
   int32_t prefold;      /* -1 auto; 0 / 1 two-level per-job Miller fold */
   int32_t lines;        /* -1 auto; 0 / 1 fixed-argument lines (bulk mode, one-lane loop) */
   int32_t defer_pct;    /* -1 auto; 0..100: share of the G2 subgroup checks run beside the Miller loops (bulk mode) */
@@ -267,9 +267,9 @@ int bgv_combine_final(bgv_ctx* ctx, const uint8_t* millers576, uint32_t n, int32
  * the textbook final exponentiation f^((p^12 - 1)/r) (the hard-part chain
  * computes 3 (p^4 - p^2 + 1)/r).  Any pointer may be NULL.
  *   pair_fe[n_sets + n_jobs]: FE of every Miller value: set pairs first
- *   (with two pairs per Miller work item, n_sets >= 65,536 or BGV_PAIRS=2,
- *   entry 2k holds the item's product and 2k+1 the identity), then each
- *   job's (-G1, S_job) pair. */
+ *   (with P = 2 or 4 pairs per Miller work item, bgv_stats.pairs_per_item,
+ *   the item's first entry, job offset + P k, holds the item's product and
+ *   the other P - 1 the identity), then each job's (-G1, S_job) pair. */
 typedef struct bgv_debug {
   uint8_t* sig_aff;  /* [n_sets][192] decoded signature (zero: invalid / identity) */
   uint8_t* h_aff;    /* [n_sets][192] H(m_i) */

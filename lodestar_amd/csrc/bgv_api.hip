@@ -185,7 +185,7 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
     auto lanes_ok = [](int v) { return v == 6 || v == 18 || v == 36; };
     if (k.miller != -1 && k.miller != 1 && k.miller != 2 && k.miller != 4 && !lanes_ok(k.miller)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.miller %d", k.miller);
     if (k.job_lanes != 0 && !lanes_ok(k.job_lanes)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.job_lanes %d", k.job_lanes);
-    if (k.pairs < 0 || k.pairs > 2) return fail(BGV_E_INVALID_ARG, "bgv_cfg.pairs %d", k.pairs);
+    if (k.pairs < 0 || k.pairs == 3 || k.pairs > 4) return fail(BGV_E_INVALID_ARG, "bgv_cfg.pairs %d", k.pairs);
     if (k.msm < -1 || k.msm > 4) return fail(BGV_E_INVALID_ARG, "bgv_cfg.msm %d", k.msm);
     if (k.clear_lanes != -1 && k.clear_lanes != 1 && k.clear_lanes != 3 && k.clear_lanes != 9)
       return fail(BGV_E_INVALID_ARG, "bgv_cfg.clear_lanes %d", k.clear_lanes);
@@ -199,7 +199,7 @@ int bgv_open_cfg(int device, const bgv_cfg* cfg, bgv_ctx** out) {
     if (!tri_ok(k.timing)) return fail(BGV_E_INVALID_ARG, "bgv_cfg.timing %d", k.timing);
     if (k.cu_split < -64 || k.cu_split > 64) return fail(BGV_E_INVALID_ARG, "bgv_cfg.cu_split %d (|N| <= 64 CUs)", k.cu_split);
     // two pairs per item exist only in the one-lane loop
-    if (k.pairs == 2 && k.miller != -1 && k.miller != 1)
+    if (k.pairs >= 2 && k.miller != -1 && k.miller != 1)
       return fail(BGV_E_INVALID_ARG, "bgv_cfg.pairs 2 needs the one-lane Miller loop (miller %d)", k.miller);
   }
   int n = 0;
@@ -648,7 +648,7 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   // the inlined Fp12 layer: 50% 39.04 / 38.93, 75% 38.54 / 38.79, 25% 39.28 / 38.97).
   // defer_from is a multiple of 64 (wave-uniform).
   const bool deferrable = !d.split || d.msm;
-  const int pct = !deferrable ? 0 : (k.defer_pct >= 0 ? k.defer_pct : (!d.split && d.pairs_per_item == 2 ? 75 : 100));
+  const int pct = !deferrable ? 0 : (k.defer_pct >= 0 ? k.defer_pct : (!d.split && d.pairs_per_item >= 2 ? 75 : 100));
   d.defer_grp = pct > 0 ? 1u : 0u;
   d.defer_from = pct > 0 ? (uint32_t)(((uint64_t)n * (uint32_t)(100 - pct) / 100u) & ~63ull) : n;
   // two-level per-job fold (bgv_tail.hip) for jobs of >= 64 sets: the fold
@@ -706,7 +706,7 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   // fixed-argument lines (pairing.h miller_lines): the G2 half of the one-lane
   // Miller loop moves to the hash stream, phase 1 (C4 40.4 -> 39.5 ms); with
   // one pair per item it loses (C4/2 26.4 -> 28.5 ms)
-  d.lines = (uint32_t)(!d.split && !d.miller_coop && (k.lines >= 0 ? k.lines : d.pairs_per_item == 2));
+  d.lines = (uint32_t)(!d.split && !d.miller_coop && (k.lines >= 0 ? k.lines : d.pairs_per_item >= 2));
   // the lines take 3 x 68 Fp2 = 19.6 KB per set (1.97 GB at C4, 2.6 GB at the
   // Node pool's 2^17-set batch cap): kept only while a quarter of the free HBM
   // covers them, else the loop recomputes them (miller_loop2, same values)
@@ -717,6 +717,8 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
         (hipMemGetInfo(&free_b, &total_b) != hipSuccess || need > free_b / 4))
       d.lines = 0;
   }
+  // four pairs per item exist only over precomputed lines (miller_loop_lines4)
+  if (d.pairs_per_item == 4 && !d.lines) d.pairs_per_item = 2;
   return 0;
 }
 

@@ -1,9 +1,10 @@
 // The set-pair Miller loop kernel (k_miller), in its own translation unit:
 // it runs at 1 wave/SIMD (512-register budget, spills in AGPRs) with its Fp12
 // accumulator in LDS, which no other kernel of bgv_kernels.hip wants.
-// Work items: every job's sets taken two at a time (one shared Fp12
-// accumulator and squaring per two pairs, miller_loop2), then one item per
-// job for its (-G1, S_job) pair.  Item offsets per job come from a scan
+// Work items: every job's sets taken pairs_per_item (1, 2 or 4) at a time (one
+// shared Fp12 accumulator and squaring per item: miller_loop2 /
+// miller_loop_lines / miller_loop_lines4), then one item per job for its
+// (-G1, S_job) pair.  Item offsets per job come from a scan
 // (bgv_kernels.hip k_item_count / k_item_job).
 #ifndef BGV_FPMUL_CALL
 #ifdef BGV_MILLER_FPMUL_CALL
@@ -64,19 +65,24 @@ __global__ void __launch_bounds__(64, BGV_MILLER_WAVES) k_miller(dev_batch b, de
   if (t < n_items) {
     const uint32_t j = w.item_job[t];
     const uint32_t i1 = b.job_off[j] + b.pairs_per_item * (t - w.item_off[j]);
-    const bool two = b.pairs_per_item == 2 && i1 + 1 < b.job_off[j + 1];
-    const bool ok1 = w.pk_code[i1] == C_OK;
-    const bool ok2 = !two || w.pk_code[i1 + 1] == C_OK;
+    const uint32_t cnt = min(b.pairs_per_item, b.job_off[j + 1] - i1);  // live pairs of the item (1..4)
+    const bool two = b.pairs_per_item == 2 && cnt == 2;
+    bool ok = true;
+    for (uint32_t k = 0; k < cnt; k++) ok &= w.pk_code[i1 + k] == C_OK;
     // a parse error rejects the whole job, so its Miller values are never used;
     // signature codes are not known yet (this part overlaps ST_SIG_SCALE)
-    if (!ok1 || !ok2) fp12_one(f);
-    else if (b.lines) miller_loop_lines(f, w.lines, b.n_sets, w.rpk_aff[i1], i1, w.rpk_aff[two ? i1 + 1 : i1], i1 + 1, two);
+    if (!ok) fp12_one(f);
+    else if (b.pairs_per_item == 4) {
+      // dead pairs (cnt < 4) read a live set's line and P; their lines are forced to 1
+      const uint32_t q1 = cnt > 1 ? i1 + 1 : i1, q2 = cnt > 2 ? i1 + 2 : i1, q3 = cnt > 3 ? i1 + 3 : i1;
+      miller_loop_lines4(f, w.lines, b.n_sets, w.rpk_aff[i1], w.rpk_aff[q1], w.rpk_aff[q2], w.rpk_aff[q3], i1, q1, q2, q3, cnt);
+    } else if (b.lines) miller_loop_lines(f, w.lines, b.n_sets, w.rpk_aff[i1], i1, w.rpk_aff[two ? i1 + 1 : i1], i1 + 1, two);
     else if (two) miller_loop2(f, w.rpk_aff[i1], w.h_aff[i1], w.rpk_aff[i1 + 1], w.h_aff[i1 + 1]);
     else miller_loop(f, w.rpk_aff[i1], false, w.h_aff[i1], false);
     w.f_set[i1] = f;
-    if (two) {
+    if (cnt > 1) {
       fp12_one(f);
-      w.f_set[i1 + 1] = f;
+      for (uint32_t k = 1; k < cnt; k++) w.f_set[i1 + k] = f;
     }
   } else {
     const uint32_t j = t - n_items;

@@ -57,11 +57,11 @@ __global__ void BGV_TREE_LB k_job_f(dev_batch b, dev_work w, uint32_t span) {
 // ------------------------------------------- cooperative folds (fp12_coop.h)
 #define COOP_LB __launch_bounds__(COOP_THREADS, 2)
 
-// With two pairs per Miller item the item's value sits at the even offsets of
-// the job and every odd entry is 1 (k_miller, k_miller_kv), so the folds step
-// over the items only: at C4 that halves the per-job chain (98 -> 49 Fp12
-// products).
-__device__ __forceinline__ static uint32_t fold_step(const dev_batch& b) { return b.pairs_per_item == 2 ? 2u : 1u; }
+// With P pairs per Miller item the item's value sits at offsets P t of the job
+// and every other entry is 1 (k_miller, k_miller_kv), so the folds step over
+// the items only: at C4 that cuts the per-job chain from 98 to 49 (P = 2) or
+// 25 (P = 4) Fp12 products.
+__device__ __forceinline__ static uint32_t fold_step(const dev_batch& b) { return b.pairs_per_item ? b.pairs_per_item : 1u; }
 
 // first level of the two-level fold (few large jobs, e.g. one 64-set gossip
 // batch, and the C4 segment's 98-set blocks): workgroup (g, j) folds the job's
@@ -184,7 +184,7 @@ void launch_fp12_tail(hipStream_t st, int stage, const dev_batch& b, const dev_w
   if (stage == ST_F_TREE) {
     if (!b.n_jobs) return;
     if (span <= 256) {  // every job folds in one workgroup
-      uint32_t stride = b.pairs_per_item == 2 ? 2u : 1u;  // fold_step
+      uint32_t stride = b.pairs_per_item ? b.pairs_per_item : 1u;  // fold_step
       if (b.prefold_log2) {  // few large jobs: fold groups side by side first
         stride = 1u << b.prefold_log2;
         hipLaunchKernelGGL(k_job_prefold, dim3((span + stride - 1) / stride, b.n_jobs), ct, 0, st, b, w);

@@ -313,4 +313,49 @@ BGV_NIL void miller_loop_lines(fp12_t& f, const fp2_t* lines, uint32_t stride, c
   fp12_conj(f, f);  // x < 0
 }
 
+// a line forced to 1 (a0 = 1, a1 = b1 = 0) where `live` is false: the dummy
+// pairs of an item with fewer than four sets leave f unchanged, and every lane
+// issues the same products (no divergent tail for a job's last item)
+BGV_HD void miller_line_keep(fp2_t& a0, fp2_t& a1, fp2_t& b1, bool live) {
+  const fp2_t one = fp2_one(), zero = fp2_zero();
+  fp2_select(a0, live, a0, one);
+  fp2_select(a1, live, a1, zero);
+  fp2_select(b1, live, b1, zero);
+}
+
+// Four pairs with ONE shared accumulator over precomputed lines (pairs_per_item
+// = 4): f = prod_k f_{x,Q_k}(P_k) for the cnt (1..4) live pairs at sets
+// i[0..3] (a dead pair's index is any live set, its line is forced to 1).  Per
+// doubling step one Fp12 squaring serves four pairs instead of two, and the
+// lines enter two at a time (fp12_mul_line2): 12 + 2 x 23 Fp2 products per
+// step against 2 x (12 + 23) for two two-pair items, ~570 fewer Fp products
+// per set at C4.  The product is the same element of Fp12 as the two-pair
+// loops' (each line's factor is exact), and its final exponentiation is what
+// the stage tests compare.
+BGV_NIL void miller_loop_lines4(fp12_t& f, const fp2_t* lines, uint32_t stride, const g1a& P0, const g1a& P1,
+                                const g1a& P2, const g1a& P3, uint32_t i0, uint32_t i1, uint32_t i2, uint32_t i3,
+                                uint32_t cnt) {
+  fp2_t a0, a1, b1, c0, c1, d1;
+  fp12_one(f);
+  uint32_t s = 0;
+  for (int b = 62; b >= 0; b--) {
+    const bool add = ((BLS_X_ABS >> b) & 1ull) != 0;
+    for (int k = 0; k < (add ? 2 : 1); k++) {
+      const bool ad = k == 1;
+      if (b != 62 && !ad) fp12_sqr(f, f);
+      miller_line_at_p(a0, a1, b1, lines, stride, i0, s, ad, P0.x, P0.y);
+      miller_line_at_p(c0, c1, d1, lines, stride, i1, s, ad, P1.x, P1.y);
+      miller_line_keep(c0, c1, d1, cnt > 1);
+      fp12_mul_line2(f, f, a0, a1, b1, c0, c1, d1);
+      miller_line_at_p(a0, a1, b1, lines, stride, i2, s, ad, P2.x, P2.y);
+      miller_line_keep(a0, a1, b1, cnt > 2);
+      miller_line_at_p(c0, c1, d1, lines, stride, i3, s, ad, P3.x, P3.y);
+      miller_line_keep(c0, c1, d1, cnt > 3);
+      fp12_mul_line2(f, f, a0, a1, b1, c0, c1, d1);
+      s++;
+    }
+  }
+  fp12_conj(f, f);  // x < 0
+}
+
 }  // namespace bgv

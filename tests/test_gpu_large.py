@@ -46,6 +46,54 @@ def test_two_pair_items_batch_with_faults():
         d.close()
 
 
+@pytest.mark.parametrize("pairs", [4])
+def test_four_pair_items_ragged_jobs_with_faults(pairs):
+    """pairs_per_item = 4 (miller_loop_lines4 over precomputed lines): jobs of
+    every size mod 4 leave items of 1, 2 and 3 live pairs, whose dead pairs'
+    lines are forced to 1; faulted sets in items at every position; verdicts
+    and the retry count equal the two-pair default's"""
+    from lodestar_amd import native
+    d4 = native.Device(0, pairs=pairs, lines=1)
+    d2 = native.Device(0)
+    try:
+        for d in (d4, d2):
+            d.gen_keys(0, 4096, 7)
+        rng = np.random.default_rng(13)
+        sizes = [98, 97, 1, 2, 3, 5, 6, 7, 99, 100, 128, 4, 9, 13, 98, 98]
+        sizes += [98] * ((70000 - sum(sizes)) // 98)
+        n = sum(sizes)
+        k = 4
+        idx = rng.integers(0, 4096, size=n * k).astype(np.uint32)
+        msgs = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+        jo = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+        arrays = {"n_sets": n, "n_jobs": len(sizes), "job_offsets": jo,
+                  "pk_offsets": (np.arange(n + 1) * k).astype(np.uint32), "pk_indices": idx, "msgs": msgs}
+        bad = np.zeros(n, bool)
+        for j in (2, 4, 5, 7, 11, 13):  # a fault in a short job / at each item position
+            bad[jo[j] + (j % int(sizes[j]))] = True
+        bad[rng.choice(n, size=24, replace=False)] = True
+        sign_msgs = msgs.copy()
+        sign_msgs[bad, 5] ^= 0x80
+        sigs = np.zeros((n, 192), np.uint8)
+        d2.gen_sign(dict(arrays, msgs=sign_msgs), sigs)
+        arrays.update(sigs=sigs, sig_len=np.full(n, 96, np.uint32),
+                      scalars=rng.integers(1, 2**63, size=n, dtype=np.uint64))
+        want = [0 if bad[jo[j]:jo[j + 1]].any() else 1 for j in range(len(sizes))]
+        jr4, sc4 = d4.verify(arrays)
+        assert d4.last_stats.layout()["pairs_per_item"] == pairs and d4.last_stats.layout()["lines"] == 1
+        assert jr4.tolist() == want and (sc4 == 0).all()
+        assert d4.last_stats.batch_retries == 1
+        jr2, _ = d2.verify(arrays)
+        assert jr2.tolist() == want
+        # the clean batch passes the batch check with no retry
+        clean = dict(arrays, msgs=sign_msgs)
+        jr4c, _ = d4.verify(clean)
+        assert jr4c.tolist() == [1] * len(sizes) and d4.last_stats.batch_retries == 0
+    finally:
+        d4.close()
+        d2.close()
+
+
 def test_many_jobs_batch_fold_and_fold_boundary():
     """2,100 single-set jobs: the batch product folds by 32 three times
     (2100 -> 66 -> 3 -> 1, ping-ponging f_batch and f_tmp); a job of exactly

@@ -36,6 +36,9 @@ MODES = {
     "bulk": {"split": 0},
     "bulk_serial_msm": {"split": 0, "miller": 1, "msm": 1, "pairs": 1},
     "c4_path": {"split": 0, "miller": 1, "msm": 2, "pairs": 2},
+    # four pairs per item over precomputed lines (miller_loop_lines4); the golden
+    # jobs' sizes leave items of 1-3 live pairs (dummy lines forced to 1)
+    "c4_path_pairs4": {"split": 0, "miller": 1, "msm": 2, "pairs": 4, "lines": 1},
     "bulk_msm4": {"split": 0, "miller": 1, "msm": 4, "pairs": 1},
     # two-pair Miller loop in Karatsuba views (miller_kv.h), 9 and 18 lanes per two pairs
     "kv3_clear3_msm4": {"split": 1, "miller_kv": 3, "msm": 4, "clear_lanes": 3},
@@ -87,11 +90,10 @@ def test_stage_values_match_oracle(golden, mode):
     # set pairs: one Miller value per set, or (two pairs per work item) the
     # item's product at its first set and the identity at its second; an item
     # with a rejected pubkey contributes the identity
-    pairs = MODES[mode].get("pairs", 1) == 2 or MODES[mode].get("miller_kv", 0) > 0
+    step = 2 if MODES[mode].get("miller_kv", 0) > 0 else MODES[mode].get("pairs", 1)
     jo = arrays["job_offsets"]
     for j in range(J):
         beg, end = int(jo[j]), int(jo[j + 1])
-        step = 2 if pairs else 1
         for i in range(beg, end, step):
             grp = list(range(i, min(i + step, end)))
             want = B.F12_ONE

@@ -11,7 +11,7 @@
 namespace bgv { unsigned long long bgv_fpmul_count = 0; }
 using namespace bgv;
 
-static int lines_mismatch = 0;
+static int lines_mismatch = 0, lines4_mismatch = 0;
 static uint64_t rng = 0x243f6a8885a308d3ull;
 static uint64_t rnd64() { rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17; return rng; }
 
@@ -30,7 +30,7 @@ int main(int argc, char** argv) {
     for (int i = 0; i < 64; i++) { jac_dbl(acc, acc); jac_add(acc, acc, g); jac_to_aff(pts[i], acc); } }
 
   const int reps = 64;
-  double sig_c = 0, sig_dec_c = 0, hash_c = 0, pk_add_c = 0, pk_fix_c = 0, sig_scale_c = 0, miller_c = 0, miller2_c = 0, lines_c = 0, loopl2_c = 0, fmul_c = 0, g2add_c = 0, aff2_c = 0, fe_c = 0;
+  double sig_c = 0, sig_dec_c = 0, hash_c = 0, pk_add_c = 0, pk_fix_c = 0, sig_scale_c = 0, miller_c = 0, miller2_c = 0, lines_c = 0, loopl2_c = 0, loopl4_c = 0, fmul_c = 0, g2add_c = 0, aff2_c = 0, fe_c = 0;
   for (int r = 0; r < reps; r++) {
     uint64_t sc = rnd64() | (1ull << 63);  // full 64-bit random scalar (top bit set: worst case)
     sc = rnd64(); if (!sc) sc = 1;
@@ -74,6 +74,32 @@ int main(int argc, char** argv) {
     fp12_t f3; miller_loop_lines(f3, lines, 1, rpa, 0, rpa, 0, true);
     loopl2_c += bgv_fpmul_count;
     if (memcmp(&f3, &f2, sizeof f2) != 0) lines_mismatch++;
+    // four pairs per item (pairs_per_item = 4): four sets' lines at stride 4;
+    // f4 equals the product of the two two-pair values exactly, and an item
+    // with cnt < 4 live pairs equals the product over its live pairs
+    {
+      static fp2_t l4[3 * MILLER_STEPS * 4];
+      g2a q4[4] = {ha, hsa, ha, hsa};
+      for (int i = 0; i < 4; i++) miller_lines(l4, 4, i, q4[i]);
+      const g1a* P = &pts[(r * 4) % 60];
+      bgv_fpmul_count = 0;
+      fp12_t f4; miller_loop_lines4(f4, l4, 4, P[0], P[1], P[2], P[3], 0, 1, 2, 3, 4);
+      loopl4_c += bgv_fpmul_count;
+      fp12_t fa, fb, fab;
+      miller_loop_lines(fa, l4, 4, P[0], 0, P[1], 1, true);
+      miller_loop_lines(fb, l4, 4, P[2], 2, P[3], 3, true);
+      fp12_mul(fab, fa, fb);
+      if (memcmp(&f4, &fab, sizeof f4) != 0) lines4_mismatch++;
+      fp12_t f4c3, fc, fac;
+      miller_loop_lines4(f4c3, l4, 4, P[0], P[1], P[2], P[0], 0, 1, 2, 0, 3);  // dead fourth pair
+      miller_loop_lines(fc, l4, 4, P[2], 2, P[2], 2, false);
+      fp12_mul(fac, fa, fc);
+      if (memcmp(&f4c3, &fac, sizeof f4) != 0) lines4_mismatch++;
+      fp12_t f4c1, fd;
+      miller_loop_lines4(f4c1, l4, 4, P[1], P[1], P[1], P[1], 1, 1, 1, 1, 1);
+      miller_loop_lines(fd, l4, 4, P[1], 1, P[1], 1, false);
+      if (memcmp(&f4c1, &fd, sizeof f4) != 0) lines4_mismatch++;
+    }
     bgv_fpmul_count = 0;
     fp12_t g; fp12_mul(g, f, f);
     fmul_c += bgv_fpmul_count;
@@ -112,7 +138,7 @@ int main(int argc, char** argv) {
     g2a sa; jac_to_aff(sa, s);
     msm_c = (double)bgv_fpmul_count / per_block;
   }
-  sig_c /= reps; sig_dec_c /= reps; hash_c /= reps; pk_add_c /= reps; pk_fix_c /= reps; sig_scale_c /= reps; miller_c /= reps; miller2_c /= reps; lines_c /= reps; loopl2_c /= reps;
+  sig_c /= reps; sig_dec_c /= reps; hash_c /= reps; pk_add_c /= reps; pk_fix_c /= reps; sig_scale_c /= reps; miller_c /= reps; miller2_c /= reps; lines_c /= reps; loopl2_c /= reps; loopl4_c /= reps;
   fmul_c /= reps; g2add_c /= reps; aff2_c /= reps;
   // C4 block mix: 95 sets of k=128, 1 of k=512, 2 singles -> mean pubkeys per set
   const double mean_k = (95.0 * k_att + k_sync + 2.0) / per_block;
@@ -143,7 +169,14 @@ int main(int argc, char** argv) {
   printf(" \"g2_decompress_only\": %.1f,\n", sig_dec_c);
   printf(" \"per_set_lines\": {\"miller_lines\": %.1f, \"miller_loop\": %.1f, \"loop_values_match\": %s},\n",
          lines_c, loopl2_c / 2.0, lines_mismatch ? "false" : "true");
+  // four pairs per item (C4 blocks of 98 sets: 24 items of 4 and one of 2,
+  // whose dead pairs still cost a full item): per set = loop4 x 25 / 98
+  printf(" \"per_set_lines4\": {\"miller_lines\": %.1f, \"miller_loop\": %.1f, \"miller_loop_full_items\": %.1f, "
+         "\"miller_product_tree\": %.1f, \"loop_values_match\": %s},\n",
+         lines_c, loopl4_c * 25.0 / per_block, loopl4_c / 4.0, fmul_c * 25.0 / per_block, lines4_mismatch ? "false" : "true");
   printf(" \"per_set_total\": %.1f,\n", sig_c + hash_c + pk_c + msm_c + miller_set + miller_jobs + f_tree);
-  printf(" \"per_set_total_lines\": %.1f\n}\n", sig_c + hash_c + pk_c + msm_c + lines_c + loopl2_c / 2.0 + miller_jobs + f_tree);
+  printf(" \"per_set_total_lines\": %.1f,\n", sig_c + hash_c + pk_c + msm_c + lines_c + loopl2_c / 2.0 + miller_jobs + f_tree);
+  printf(" \"per_set_total_lines4\": %.1f\n}\n", sig_c + hash_c + pk_c + msm_c + lines_c + loopl4_c * 25.0 / per_block + miller_jobs +
+         fmul_c * 25.0 / per_block);
   return 0;
 }
