@@ -337,16 +337,39 @@ def mixed_sizes(d, darr, reps: int = 4):
             "reps": reps, "note": "C2 and C4 batches alternated on one context"}
 
 
-def epoch_slice(d, torch, dev, arrays_host: dict, sigs, blocks: int = 32, reps: int = 7):
+def epoch_slice(d, torch, dev, arrays_host: dict, sigs, blocks: int = 32, reps: int = 7, ds=None):
     """One epoch of the segment (32 blocks = 3,136 sets): the batch a range
-    sync hands the verifier per epoch (sync/constants.ts:41), on device, p50"""
-    from lodestar_amd.dist import select_jobs
+    sync hands the verifier per epoch (sync/constants.ts:41), on device, p50;
+    with `ds`, also the pace of a stream of such batches with len(ds) in flight
+    (the pool's contexts per device)"""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from lodestar_amd.dist import run_in_flight, select_jobs
     sub = select_jobs(dict(arrays_host, sigs=sigs), list(range(blocks)))
     da = to_device(sub, torch, dev)
     da.update(sig_len=torch.full((sub["n_sets"],), 96, dtype=torch.int32, device=dev), scalars=None)
     p50 = p50_latency(d, da, reps=reps, on_device=True)
-    return {"sets": int(sub["n_sets"]), "blocks": blocks, "p50_ms": p50, "sets_per_s": round(sub["n_sets"] / p50 * 1e3, 1),
-            "layout": d.last_stats.layout()}
+    out = {"sets": int(sub["n_sets"]), "blocks": blocks, "p50_ms": p50, "sets_per_s": round(sub["n_sets"] / p50 * 1e3, 1),
+           "layout": d.last_stats.layout()}
+    if ds and len(ds) > 1:
+        ex = ThreadPoolExecutor(max_workers=len(ds))
+
+        def submit(k):
+            return ex.submit(ds[k % len(ds)].verify, da, on_device=True, want_set_codes=False)
+
+        def finish(k, res):
+            return bool((res[0] == 1).all())
+
+        n = 8 * len(ds)
+        assert run_in_flight(submit, finish, len(ds), len(ds))
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        assert run_in_flight(submit, finish, n, len(ds))
+        ms = (time.perf_counter() - t1) / n * 1e3
+        ex.shutdown()
+        out.update(ms_per_batch_in_flight=round(ms, 3), inflight=len(ds),
+                   sets_per_s_in_flight=round(sub["n_sets"] / ms * 1e3, 1))
+    return out
 
 
 def host_resident_c4(d, arrays_host: dict, reps: int = 3):
@@ -680,7 +703,7 @@ def main():
         host["sig_len"] = np.full(n_sets, 96, np.uint32)
         host["scalars"] = None
         legs["c4_host_resident"] = host_resident_c4(d, host)
-        legs["c4_epoch_slice"] = epoch_slice(d, torch, dev, arrays, host["sigs"])
+        legs["c4_epoch_slice"] = epoch_slice(d, torch, dev, arrays, host["sigs"], ds=ds)
         legs["mixed_sizes"] = mixed_sizes(d, darr)
         if world == 1:
             legs["strong_shard_projection"] = shard_projection(d, torch, dev, host, ds)

@@ -62,6 +62,42 @@ LAYOUT = {256: {"split": 1, "miller_lanes": 2, "msm": 4, "clear_lanes": 1},
           608: {"split": 0, "miller_lanes": 1, "pairs_per_item": 1, "msm": 2}}
 
 
+def test_faulted_shard_on_reserved_bulk_context():
+    """the C4/8 shard (128 blocks, 1 % faults of the four C5 kinds) on a bulk
+    context that leaves 32 CUs to a priority context (bgv_cfg.cu_split = -32,
+    device 0 of the pools when CUs are reserved), beside a priority context
+    (cu_split = +32) verifying a faulted one-block batch at the same time:
+    every verdict and set code as constructed on both"""
+    import threading
+
+    from lodestar_amd import native
+    bulk = native.Device(0, cu_split=-32)
+    prio = native.Device(0, cu_split=32)
+    try:
+        for d in (bulk, prio):
+            d.gen_keys(0, N_TABLE, SEED)
+        a = bench.build_segment(list(range(128)), seed=SEED + 7500)
+        fa, expect, code = bench.inject_faults(bulk, a, 0.01, SEED + 7600, with_codes=True)
+        one = bench.build_segment([0], seed=SEED + 7700)
+        fo, expect1, code1 = bench.inject_faults(prio, one, 0.05, SEED + 7800, with_codes=True)
+        out = {}
+
+        def run_prio():
+            out["prio"] = prio.verify(fo)
+
+        t = threading.Thread(target=run_prio)
+        t.start()
+        jr, sc = bulk.verify(fa)
+        t.join()
+        assert jr.tolist() == expect.tolist() and sc.tolist() == code.tolist()
+        assert bulk.last_stats.batch_retries == 1
+        jr1, sc1 = out["prio"]
+        assert jr1.tolist() == expect1.tolist() and sc1.tolist() == code1.tolist()
+    finally:
+        bulk.close()
+        prio.close()
+
+
 @pytest.mark.parametrize("blocks", sorted(SIZES))
 def test_faulted_shard_default_layout(dev, blocks):
     from lodestar_amd.dist import batch_job_work, select_jobs, shard_jobs
