@@ -14,12 +14,15 @@ drawn (device ChaCha20 keyed by getrandom) and applied, one Miller loop per
 set, per-block products,
 and the final exponentiation (one for the segment; per-block ones only if
 it fails).  Inputs (indices, messages, signatures) are resident in HBM
-before the timed region.  --inflight D (default 3) batches are in flight per
-GPU, one context each, as a pool with D contexts per device runs them: the
-next batches' phase 1 fills the SIMDs a batch's Miller phase leaves idle.  Multi-GPU (weak scaling): every rank verifies its
-own 32-epoch segment (seeded per rank); each reduces its segment to one
-Fp12 Miller product, the 576-byte partials are all-gathered over RCCL and
-the node's ONE final exponentiation runs on their product.
+before the timed region.  --inflight D batches are in flight per GPU (auto:
+3, or 4 when a GPU's batch is under 32,000 sets, i.e. the strong-scaling
+shards of N >= 4), one context each, as a pool with D contexts per device
+runs them: the next batches' phase 1 fills the SIMDs a batch's Miller phase
+leaves idle.  Multi-GPU (default, strong scaling): ONE segment split by job
+over the ranks (dist.shard_jobs); each rank reduces its shard to one Fp12
+Miller product, the 576-byte partials are all-gathered over RCCL and ONE
+final exponentiation runs on their product, then the per-block verdicts are
+all-gathered.  --weak: every rank verifies its own segment.
 A second measurement times the gossip batch (BASELINE configs[1], "C2":
 64 aggregate sets x 128 pubkeys, batchable, one job) for the p50 latency.
 
@@ -51,8 +54,11 @@ SEED = 0x4C4F4445
 # batches in flight per GPU (one context each): the next batches' hash, pubkey
 # and decode kernels fill the SIMDs a batch's one-wave Miller phase leaves idle
 # (profiles/r06b_overlap_sizes.txt: C4 36.7 -> 34.2 / 33.1 ms per batch with
-# 2 / 3 in flight; C4/8 9.65 -> 8.35 / 7.59 ms with 3 / 4)
+# 2 / 3 in flight, 34.0 with 4; C4/8 9.65 -> 8.35 / 7.59 ms with 3 / 4): three
+# for batches of >= 32,000 sets per GPU, four below (the shards of N >= 4)
 INFLIGHT = 3
+INFLIGHT_SMALL = 4
+INFLIGHT_SMALL_BELOW = 32000
 
 
 def log(*a):
@@ -556,12 +562,13 @@ def main():
     ap.add_argument("--weak", action="store_true",
                     help="N > 1: every rank verifies its own segment (default: ONE segment split across the ranks, BASELINE configs[3])")
     ap.add_argument("--no-weak-leg", action="store_true", help="N > 1: skip the extra weak-scaling measurement")
-    ap.add_argument("--inflight", type=int, default=INFLIGHT,
-                    help="batches in flight per GPU: contexts on the GPU, one worker thread each (dist.run_in_flight)")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="batches in flight per GPU: contexts on the GPU, one worker thread each (dist.run_in_flight); "
+                         "0 = auto (3, or 4 for batches under 32,000 sets per GPU)")
     ap.add_argument("--cfg", action="append", default=[], metavar="KEY=VAL",
                     help="bgv_cfg override for every context (A/B runs only, e.g. pairs=4)")
     args = ap.parse_args()
-    assert args.inflight >= 1
+    assert args.inflight >= 0
     cfg = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in args.cfg}
 
     import torch
@@ -597,6 +604,9 @@ def main():
     log(f"[bench] {N_VALIDATORS} keys generated in {time.time() - t0:.1f}s")
     # the other contexts of the batches in flight: each holds its own table
     # replica (as every context of the pools does) and its own streams
+    if not args.inflight:
+        per_gpu = args.blocks * SETS_PER_BLOCK // (world if (world > 1 and not args.weak) else 1)
+        args.inflight = INFLIGHT_SMALL if per_gpu < INFLIGHT_SMALL_BELOW else INFLIGHT
     ds = [d]
     for _ in range(args.inflight - 1):
         x = native.Device(gpu, **cfg)
