@@ -48,6 +48,16 @@
 #ifndef BGV_MILLER_LDS_F
 #define BGV_MILLER_LDS_F 1
 #endif
+// The Fp2 leaf (fp2.h BGV_FP2_LEAF) stays off in this unit: its 48-dword
+// argument frame pushes k_hash over the 256-register line of two waves per
+// SIMD (k_hash 16.0 -> 17.7 ms alone; profiles/r06i_fp2_leaf/).  The Miller
+// and latency units take it.  BGV_KERNELS_FP2_LEAF=1 builds the A/B variant.
+#ifndef BGV_KERNELS_FP2_LEAF
+#define BGV_KERNELS_FP2_LEAF 0
+#endif
+#ifndef BGV_FP2_LEAF
+#define BGV_FP2_LEAF BGV_KERNELS_FP2_LEAF
+#endif
 #include "bgv_internal.h"
 #include "miller_coop.h"
 

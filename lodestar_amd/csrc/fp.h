@@ -310,6 +310,43 @@ BGV_HD void fp_mul28(fp_t& r, const fp_t& a, const fp_t& b) {
   fp_reduce_once(r, t);
 }
 
+// Sum of two products with ONE Montgomery reduction, on pre-split digits:
+// r = (a b + c d) 2^-384 mod p with A = digits(a << 8), C = digits(c << 8),
+// B = digits(b), D = digits(d).  Column bound: 28 digit products < 2^60.8 +
+// 14 reduction terms < 2^59.8 + carry < 2^62.  Output before the final
+// subtraction < (a b + c d) / 2^384 + p, canonical after it whenever
+// a b + c d < 2^384 p (e.g. every operand < 2p: 8 p^2 < 2^384 p).  The Fp2
+// product below computes each coefficient this way: the same 4 x 196 + 2 x 196
+// digit products as three Karatsuba products, with two unpack/pack/final
+// subtractions instead of three and no Karatsuba additions.
+BGV_HD void fp_mulsum28_digits(fp_t& r, const uint32_t A[14], const uint32_t B[14], const uint32_t C[14], const uint32_t D[14]) {
+  uint64_t acc[28];
+#pragma unroll
+  for (int k = 0; k < 28; k++) acc[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++)
+#pragma unroll
+    for (int j = 0; j < 14; j++) acc[i + j] += (uint64_t)A[i] * B[j] + (uint64_t)C[i] * D[j];
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    const uint32_t m = ((uint32_t)acc[i] * P28_INV) & M28;
+#pragma unroll
+    for (int j = 0; j < 14; j++) acc[i + j] += (uint64_t)m * P28[j];
+    acc[i + 1] += acc[i] >> 28;
+  }
+  uint32_t d[14];
+  uint64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 14; k++) {
+    const uint64_t v = acc[14 + k] + c;
+    d[k] = (uint32_t)v & M28;
+    c = v >> 28;
+  }
+  fp_t t;
+  pack28(t, d);
+  fp_reduce_once(r, t);
+}
+
 // Squaring on the same digits: both operands are a << 4, so the square
 // carries the 2^8 of the pre-shift; the 91 cross products are summed once
 // against a doubled digit (2 A_j < 2^29), 105 digit products instead of 196.

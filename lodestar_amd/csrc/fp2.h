@@ -95,20 +95,84 @@ BGV_HD void fp2_mul3(fp2_t& r, const fp2_t& a) { fp2_t t; fp2_dbl(t, a); fp2_add
 BGV_HD void fp2_mul4(fp2_t& r, const fp2_t& a) { fp2_t t; fp2_dbl(t, a); fp2_dbl(r, t); }
 BGV_HD void fp2_mul8(fp2_t& r, const fp2_t& a) { fp2_t t; fp2_dbl(t, a); fp2_dbl(t, t); fp2_dbl(r, t); }
 
-// Karatsuba: 3 Fp products
-BGV_NI2 void fp2_mul(fp2_t& r, const fp2_t& a, const fp2_t& b) {
-  fp_t t0, t1, t2, t3;
-  fp_mul(t0, a.c0, b.c0);
-  fp_mul(t1, a.c1, b.c1);
-  fp_add_lazy2(t2, a.c0, a.c1, t3, b.c0, b.c1);  // < 2p, product inputs only
-  fp_mul(t2, t2, t3);
-  fp_sub2(r.c0, t0, t1, t2, t2, t0);
-  fp_sub(r.c1, t2, t1);
+// The Fp2 product as two sums of products, one Montgomery reduction each
+// (fp_mulsum28_digits): c0 = a0 b0 + (2p - a1) b1, c1 = a0 b1 + a1 b0, for
+// operands < 2p.  The digit products are those of three Karatsuba products;
+// what goes is one unpack / pack / final subtraction and the five Karatsuba
+// additions (the leaf is ~1,700 instructions against ~1,950 for three Fp
+// leaves and their additions, tools/ubench_fp2.hip).  The result is the
+// canonical product, bit-identical to Karatsuba's.
+BGV_HD void fp2_mul_sop(fp2_t& r, const fp2_t& a, const fp2_t& b) {
+  fp_t na1;  // 2p - a1, no reduction (a1 <= 2p)
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    const uint32_t p2 = (P_MOD.l[i] << 1) | (i ? P_MOD.l[i - 1] >> 31 : 0u);
+    na1.l[i] = subb32(p2, a.c1.l[i], br, br);
+  }
+  uint32_t A0[14], A1[14], N1[14], B0[14], B1[14];
+  unpack28<8>(A0, a.c0);
+  unpack28<8>(A1, a.c1);
+  unpack28<8>(N1, na1);
+  unpack28<0>(B0, b.c0);
+  unpack28<0>(B1, b.c1);
+  fp_t c0, c1;
+  fp_mulsum28_digits(c0, A0, B0, N1, B1);
+  fp_mulsum28_digits(c1, A0, B1, A1, B0);
+  r.c0 = c0;
+  r.c1 = c1;
 }
 
-// force-inlined copy for call sites that want the three products scheduled
-// together with their neighbours (Fp6 multiplications, see fp12.h)
-BGV_HD void fp2_mul_inl(fp2_t& r, const fp2_t& a, const fp2_t& b) {
+// BGV_FP2_LEAF: on the device, every Fp2 product of a unit that calls its
+// products (BGV_FPMUL_CALL) is ONE call to this leaf.  Its 48 argument dwords
+// exceed the 32 argument VGPRs of the calling convention, so b.c1 travels on
+// the stack; the result comes back in v0-v23.
+#ifndef BGV_FP2_LEAF
+#define BGV_FP2_LEAF 1
+#endif
+#if defined(__HIPCC__) && BGV_FPMUL_CALL && BGV_FP2_LEAF
+typedef uint32_t fp2_vec_t __attribute__((ext_vector_type(24)));
+static __device__ __noinline__ fp2_vec_t fp2_mul_leaf(fp_vec_t a0, fp_vec_t a1, fp_vec_t b0, fp_vec_t b1) {
+  fp2_t a, b, r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    a.c0.l[i] = a0[i];
+    a.c1.l[i] = a1[i];
+    b.c0.l[i] = b0[i];
+    b.c1.l[i] = b1[i];
+  }
+  fp2_mul_sop(r, a, b);
+  fp2_vec_t v;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    v[i] = r.c0.l[i];
+    v[NL + i] = r.c1.l[i];
+  }
+  return v;
+}
+#endif
+
+BGV_HD void fp2_mul_body(fp2_t& r, const fp2_t& a, const fp2_t& b) {
+#if defined(__HIP_DEVICE_COMPILE__) && BGV_FPMUL_CALL && BGV_FP2_LEAF
+#ifdef BGV_COUNT_OPS
+  bgv_fpmul_count += 3;
+#endif
+  fp_vec_t a0, a1, b0, b1;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    a0[i] = a.c0.l[i];
+    a1[i] = a.c1.l[i];
+    b0[i] = b.c0.l[i];
+    b1[i] = b.c1.l[i];
+  }
+  const fp2_vec_t v = fp2_mul_leaf(a0, a1, b0, b1);
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    r.c0.l[i] = v[i];
+    r.c1.l[i] = v[NL + i];
+  }
+#else
+  // Karatsuba: 3 Fp products
   fp_t t0, t1, t2, t3;
   fp_mul(t0, a.c0, b.c0);
   fp_mul(t1, a.c1, b.c1);
@@ -116,7 +180,14 @@ BGV_HD void fp2_mul_inl(fp2_t& r, const fp2_t& a, const fp2_t& b) {
   fp_mul(t2, t2, t3);
   fp_sub2(r.c0, t0, t1, t2, t2, t0);
   fp_sub(r.c1, t2, t1);
+#endif
 }
+
+BGV_NI2 void fp2_mul(fp2_t& r, const fp2_t& a, const fp2_t& b) { fp2_mul_body(r, a, b); }
+
+// force-inlined copy for call sites that want the products scheduled
+// together with their neighbours (Fp6 multiplications, see fp12.h)
+BGV_HD void fp2_mul_inl(fp2_t& r, const fp2_t& a, const fp2_t& b) { fp2_mul_body(r, a, b); }
 
 // complex squaring: 2 Fp products
 BGV_NI2 void fp2_sqr(fp2_t& r, const fp2_t& a) {

@@ -41,6 +41,53 @@ void hc_fp2_sqr(const uint8_t* a, uint8_t* out) { fp2_t x, z; get_fp2(x, a); fp2
 void hc_fp2_inv(const uint8_t* a, uint8_t* out) { fp2_t x, z; get_fp2(x, a); fp2_inv(z, x); put_fp2(out, z); }
 // fp_mul on unreduced inputs a + p, b + p (< 2p, the fp_add_lazy range) must
 // return the same canonical limbs as on a, b; returns the number of failures
+void hc_fp2_mul_sop(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  fp2_t x, y, z; get_fp2(x, a); get_fp2(y, b); fp2_mul_sop(z, x, y); put_fp2(out, z);
+}
+
+// the sum-of-products Fp2 product (fp2_mul_sop, the device's Fp2 leaf) against
+// Karatsuba on canonical operands and on lazy ones (x + p < 2p in any
+// component, and the extremes p - 1, 2p - 1): bit-identical canonical output
+int hc_sop_lazy_check(uint64_t seed, int n) {
+  uint64_t x = seed | 1;
+  auto rnd = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+  auto canon = [&](fp_t& a) {
+    for (int i = 0; i < NL; i++) a.l[i] = (uint32_t)rnd();
+    a.l[NL - 1] &= 0x1fffffffu;
+    fp_reduce_once(a, a); fp_reduce_once(a, a);
+    if (!fp_plain_lt_p(a)) fp_sub(a, a, P_MOD);
+  };
+  auto lazy = [&](fp_t& r, const fp_t& a) {
+    uint64_t c = 0;
+    for (int i = 0; i < NL; i++) { c += (uint64_t)a.l[i] + P_MOD.l[i]; r.l[i] = (uint32_t)c; c >>= 32; }
+  };
+  int bad = 0;
+  for (int it = 0; it < n; it++) {
+    fp2_t a, b;
+    canon(a.c0); canon(a.c1); canon(b.c0); canon(b.c1);
+    if (it < 4) { a.c1 = P_MOD; a.c1.l[0] -= 1; b.c1 = a.c1; }  // p - 1
+    if (it == 1) fp_set_zero(a.c1);
+    fp2_t k, s, al, bl, sl;
+    const uint32_t sel = (uint32_t)rnd();
+    al = a; bl = b;
+    if (sel & 1) lazy(al.c0, a.c0);
+    if (sel & 2) lazy(al.c1, a.c1);
+    if (sel & 4) lazy(bl.c0, b.c0);
+    if (sel & 8) lazy(bl.c1, b.c1);
+    if (it == 2) { lazy(al.c0, a.c0); lazy(al.c1, a.c1); lazy(bl.c0, b.c0); lazy(bl.c1, b.c1); }  // 2p - 1 everywhere
+    // Karatsuba on the canonical values (the host path of fp2_mul)
+    fp_t t0, t1, t2, t3;
+    fp_mul(t0, a.c0, b.c0); fp_mul(t1, a.c1, b.c1);
+    fp_add_lazy2(t2, a.c0, a.c1, t3, b.c0, b.c1); fp_mul(t2, t2, t3);
+    fp_sub2(k.c0, t0, t1, t2, t2, t0); fp_sub(k.c1, t2, t1);
+    fp2_mul_sop(s, a, b);
+    fp2_mul_sop(sl, al, bl);
+    if (memcmp(&k, &s, sizeof k) || memcmp(&k, &sl, sizeof k)) bad++;
+    if (!fp_plain_lt_p(sl.c0) || !fp_plain_lt_p(sl.c1)) bad++;
+  }
+  return bad;
+}
+
 int hc_lazy_mul_canonical(uint64_t seed, int n) {
   uint64_t x = seed | 1;
   auto rnd = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };

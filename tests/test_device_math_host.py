@@ -67,6 +67,14 @@ def test_fp2_ops():
         assert B.f2_eq(B.f2_mul(H.b_fp2(o.raw), a), B.F2_ONE)
         assert lib.hc_fp2_sgn0(H.fp2_b(a)) == B.f2_sgn0(a)
     assert lib.hc_lazy_mul_canonical(ctypes.c_uint64(12345), 20000) == 0
+    # the sum-of-products Fp2 product (the device's Fp2 leaf): against the oracle,
+    # and bit-identical to Karatsuba on canonical and lazy (< 2p) operands
+    for _ in range(50):
+        a, b = rfp2(), rfp2()
+        o = H.buf(96)
+        lib.hc_fp2_mul_sop(H.fp2_b(a), H.fp2_b(b), o)
+        assert H.b_fp2(o.raw) == B.f2_mul(a, b)
+    assert lib.hc_sop_lazy_check(ctypes.c_uint64(777), 20000) == 0
     # lazy Karatsuba sums (fp_add_lazy, < 2p): Montgomery images at p-1, p-2 make them largest
     rinv = pow(2**384, -1, B.P)
     hi = [(B.P - k) * rinv % B.P for k in (1, 2, 3)] + [B.P - 1, 1, 0, (B.P - 1) // 2 * rinv % B.P]
