@@ -378,9 +378,11 @@ def epoch_slice(d, torch, dev, arrays_host: dict, sigs, blocks: int = 32, reps: 
     return out
 
 
-def host_resident_c4(d, arrays_host: dict, reps: int = 3):
+def host_resident_c4(d, arrays_host: dict, reps: int = 3, ds=None):
     """C4 with every input in host memory: the pinned staging copy and the
-    PCIe transfer are inside the timed region (the path a Node caller takes)"""
+    PCIe transfer are inside the timed region (the path a Node caller takes);
+    with `ds`, also len(ds) such batches in flight (the Node pool's contexts
+    per device: each stages and copies its own batch)"""
     d.verify(arrays_host, want_set_codes=False)
     t = []
     for _ in range(reps):
@@ -389,9 +391,30 @@ def host_resident_c4(d, arrays_host: dict, reps: int = 3):
         t.append(time.perf_counter() - t1)
         assert (jr == 1).all()
     ms = float(np.median(t)) * 1e3
-    return {"ms_per_step": round(ms, 3), "sets_per_s": round(arrays_host["n_sets"] / ms * 1e3, 1),
-            "h2d_bytes": int(arrays_host["n_sets"] * (32 + 192 + 4) + arrays_host["pk_indices"].nbytes
-                             + arrays_host["pk_offsets"].nbytes + arrays_host["job_offsets"].nbytes)}
+    out = {"ms_per_step": round(ms, 3), "sets_per_s": round(arrays_host["n_sets"] / ms * 1e3, 1),
+           "h2d_bytes": int(arrays_host["n_sets"] * (32 + 192 + 4) + arrays_host["pk_indices"].nbytes
+                            + arrays_host["pk_offsets"].nbytes + arrays_host["job_offsets"].nbytes)}
+    if ds and len(ds) > 1:
+        from concurrent.futures import ThreadPoolExecutor
+
+        from lodestar_amd.dist import run_in_flight
+        ex = ThreadPoolExecutor(max_workers=len(ds))
+
+        def submit(k):
+            return ex.submit(ds[k % len(ds)].verify, arrays_host, want_set_codes=False)
+
+        def finish(k, res):
+            return bool((res[0] == 1).all())
+
+        n = 3 * len(ds)
+        assert run_in_flight(submit, finish, len(ds), len(ds))
+        t1 = time.perf_counter()
+        assert run_in_flight(submit, finish, n, len(ds))
+        mi = (time.perf_counter() - t1) / n * 1e3
+        ex.shutdown()
+        out.update(ms_per_batch_in_flight=round(mi, 3), inflight=len(ds),
+                   sets_per_s_in_flight=round(arrays_host["n_sets"] / mi * 1e3, 1))
+    return out
 
 
 def shard_projection(d, torch, dev, arrays_host: dict, ds=None, worlds=(2, 4, 8), reps: int = 5):
@@ -712,7 +735,7 @@ def main():
         host["sigs"] = sigs.cpu().numpy()
         host["sig_len"] = np.full(n_sets, 96, np.uint32)
         host["scalars"] = None
-        legs["c4_host_resident"] = host_resident_c4(d, host)
+        legs["c4_host_resident"] = host_resident_c4(d, host, ds=ds)
         legs["c4_epoch_slice"] = epoch_slice(d, torch, dev, arrays, host["sigs"], ds=ds)
         legs["mixed_sizes"] = mixed_sizes(d, darr)
         if world == 1:
