@@ -1,14 +1,18 @@
 // Design study (not part of the library): the Fp2 product as Karatsuba over
 // the library's Fp leaf (3 calls, 2 lazy additions, 3 modular subtractions)
 // against ONE Fp2 leaf computing each output coefficient as a sum of two
-// products with a single Montgomery reduction:
+// products with a single Montgomery reduction (fp2.h fp2_mul_sop):
 //   c0 = a0 b0 + (2p - a1) b1,  c1 = a0 b1 + a1 b0    (4 x 196 + 2 x 196 digit mads)
+// (A Karatsuba on double-width columns with one reduction per coefficient,
+// 980 digit mads, measured 4.40 us lone / 9.9 G/s: its signed 28-column
+// accumulators spill; not kept, profiles/r06j_ubench_fp2.json.)
 // The Fp2 leaf's 48 argument dwords exceed the 32 argument VGPRs of the
 // AMDGPU calling convention, so 16 travel on the stack (variant "stack"); the
 // "ptr" variant passes b by pointer.  Lone-wave latency and full-chip
 // throughput of chains of Fp2 products.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -o tools/ubench_fp2 tools/ubench_fp2.hip && ./tools/ubench_fp2
 #define BGV_FPMUL_CALL 1
+#define BGV_FP2_LEAF 0  // fp2_mul_inl stays Karatsuba over the Fp leaf (the baseline)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -17,57 +21,6 @@
 namespace bgv {
 
 typedef uint32_t fp2_vec_t __attribute__((ext_vector_type(24)));
-
-// (a b + c d) 2^-384 mod p for a, c < 2^384 pre-shifted, b, d digits; a b + c d < 2^384 p
-__device__ __forceinline__ void mulsum_core(fp_t& r, const uint32_t A[14], const uint32_t B[14], const uint32_t C[14],
-                                            const uint32_t D[14]) {
-  uint64_t acc[28];
-#pragma unroll
-  for (int k = 0; k < 28; k++) acc[k] = 0;
-#pragma unroll
-  for (int i = 0; i < 14; i++)
-#pragma unroll
-    for (int j = 0; j < 14; j++) acc[i + j] += (uint64_t)A[i] * B[j] + (uint64_t)C[i] * D[j];
-#pragma unroll
-  for (int i = 0; i < 14; i++) {
-    const uint32_t m = ((uint32_t)acc[i] * P28_INV) & M28;
-#pragma unroll
-    for (int j = 0; j < 14; j++) acc[i + j] += (uint64_t)m * P28[j];
-    acc[i + 1] += acc[i] >> 28;
-  }
-  uint32_t d[14];
-  uint64_t c = 0;
-#pragma unroll
-  for (int k = 0; k < 14; k++) {
-    const uint64_t v = acc[14 + k] + c;
-    d[k] = (uint32_t)v & M28;
-    c = v >> 28;
-  }
-  fp_t t;
-  pack28(t, d);
-  fp_reduce_once(r, t);
-}
-
-__device__ __forceinline__ void fp2_mul_sop(fp2_t& r, const fp2_t& a, const fp2_t& b) {
-  // 2p - a1 (a1 <= 2p): 12-limb subtraction, no reduction
-  fp_t na1;
-  {
-    uint32_t br = 0;
-#pragma unroll
-    for (int i = 0; i < NL; i++) {
-      const uint32_t p2 = (P_MOD.l[i] << 1) | (i ? P_MOD.l[i - 1] >> 31 : 0u);
-      na1.l[i] = subb32(p2, a.c1.l[i], br, br);
-    }
-  }
-  uint32_t A0[14], A1[14], N1[14], B0[14], B1[14];
-  unpack28<8>(A0, a.c0);
-  unpack28<8>(A1, a.c1);
-  unpack28<8>(N1, na1);
-  unpack28<0>(B0, b.c0);
-  unpack28<0>(B1, b.c1);
-  mulsum_core(r.c0, A0, B0, N1, B1);
-  mulsum_core(r.c1, A0, B1, A1, B0);
-}
 
 static __device__ __noinline__ fp2_vec_t fp2_mul_leaf_stack(fp_vec_t a0, fp_vec_t a1, fp_vec_t b0, fp_vec_t b1) {
   fp2_t a, b, r;
@@ -206,6 +159,7 @@ int main() {
   r[1] = {"fp2_leaf_stack_args", run(k_fp2_stack, d, 1, it), run(k_fp2_stack, d, big, it / 10)};
   hipMemcpy(d, h, n * 2 * sizeof(fp2_t), hipMemcpyHostToDevice);
   r[2] = {"fp2_leaf_b_by_pointer", run(k_fp2_ptr, d, 1, it), run(k_fp2_ptr, d, big, it / 10)};
+
   printf("{\"mismatches\": %u, ", hb);
   for (int k = 0; k < 3; k++) {
     const double lone_us = r[k].lone * 1e3 / it;
