@@ -100,6 +100,11 @@ const CONTEXTS_PER_DEVICE = 3;
 // (verifyBlocksSignatures.ts:30-47, sleep(0) every 8 blocks) coalesce
 const MAX_QUIET_WAITS = 8;
 const RAW_BIT = 0x80000000;
+// the G1 generator, 96-byte uncompressed, and the identity signature: the priority context's sizing job
+const G1_GENERATOR_96 = Uint8Array.from(Buffer.from(
+  "17f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb" +
+  "08b3f481e3aaa0f1a09e30ed741d8ae4fcf5e095d5d00af600db18cb2c04b3edd03cc744a2888ae40caa232946c5e7e1", "hex"));
+const IDENTITY_SIG_96 = (() => { const b = new Uint8Array(96); b[0] = 0xc0; return b; })();
 const EMPTY_JOB = -10; // BGV internal code: a job without sets
 
 class QueueError extends Error {
@@ -306,6 +311,7 @@ class BlsGpuVerifier {
     this.prio = blsVerifyAllMultiThread ? null : addon.open(ids[0], priorityCus > 0 ? priorityCus : 0);
     this.prioReserved = priorityCus > 0;
     this.priorityCus = priorityCus;
+    if (this.prio) this.warmPriority();
     this.prioBusy = 0;
     this.idle = this.ctxs.map(() => true);
     this.maxSetsPerDeviceBatch = maxSetsPerDeviceBatch;
@@ -332,6 +338,16 @@ class BlsGpuVerifier {
   // rows in either format (0: 48-byte compressed, 1: 96-byte uncompressed) into every replica
   pubkeysSet(firstIndex, bytes, format) {
     for (const c of this.allContexts()) addon.pubkeysSet(c, firstIndex, bytes, format);
+  }
+
+  // sizes the priority context's work buffers for a full job (128 sets) at
+  // construction, so a verifyOnMainThread call never frees and regrows them
+  // (a hipFree synchronises the device: it would wait for the bulk contexts'
+  // batches in flight).  One dummy job: the generator as a raw key and the
+  // identity signature; its verdict is ignored.
+  warmPriority() {
+    const set = {type: "single", pubkey: {raw: G1_GENERATOR_96}, signingRoot: new Uint8Array(32), signature: IDENTITY_SIG_96};
+    addon.verifySync(this.prio, encodeJobs([new Array(MAX_SIGNATURE_SETS_PER_JOB).fill(set)]));
   }
 
   allContexts() {

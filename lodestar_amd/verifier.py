@@ -55,6 +55,11 @@ PRIORITY_CUS = 32  # CUs of the first device kept for verifyOnMainThread (bgv_cf
 # CONTEXTS_PER_DEVICE): the next batches' phase 1 fills the SIMDs a batch's
 # Miller phase leaves idle (profiles/r06b_overlap_sizes.txt)
 CONTEXTS_PER_DEVICE = 3
+# the priority context's sizing job (BlsGpuVerifier._warm_priority)
+G1_GENERATOR_96 = bytes.fromhex(
+    "17f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb"
+    "08b3f481e3aaa0f1a09e30ed741d8ae4fcf5e095d5d00af600db18cb2c04b3edd03cc744a2888ae40caa232946c5e7e1")
+IDENTITY_SIG_96 = bytes([0xC0]) + bytes(95)
 MAX_SETS_PER_DEVICE_BATCH = 1 << 17
 # a device batch of at least this many sets (and >= 2 jobs) is split by job
 # over the idle devices: each returns a partial Miller product and ONE final
@@ -334,6 +339,8 @@ class BlsGpuVerifier:
         else:
             self.prio = native.Device(devices[0], cu_split=priority_cus) if priority_cus > 0 else native.Device(devices[0])
         self.prio_reserved = priority_cus > 0  # device 0's bulk context runs at RESERVED_CAP (shard_jobs caps)
+        if self.prio is not None:
+            self._warm_priority()
         self._prio_lock = threading.Lock()
         self._shard_min = shard_min_sets
         self._idle = [True] * len(self.devices)
@@ -510,6 +517,16 @@ class BlsGpuVerifier:
         self.metrics["batch_retries"] += int(st.batch_retries)
         self.metrics["batch_sigs_success"] += int(st.batch_sigs_success)
         self.metrics["device_time_s"] += seconds
+
+    def _warm_priority(self):
+        """sizes the priority context's work buffers for a full job (128 sets)
+        at construction, so a verifyOnMainThread call never frees and regrows
+        them (a hipFree synchronises the device and would wait for the bulk
+        contexts' batches).  One dummy job: the G1 generator as a raw key and
+        the identity signature; its verdict is ignored."""
+        one = create_single_signature_set_from_components(PublicKey(raw=G1_GENERATOR_96), bytes(32), IDENTITY_SIG_96)
+        self.prio.verify(encode_jobs([[one] * MAX_SIGNATURE_SETS_PER_JOB], np.ones(MAX_SIGNATURE_SETS_PER_JOB, np.uint64)),
+                         want_set_codes=False)
 
     def _contexts(self) -> list:
         return self.devices + ([self.prio] if self.prio is not None else [])

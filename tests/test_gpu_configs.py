@@ -171,7 +171,8 @@ def test_c3_blocks_first_invalid(coalesce, att_k):
 
 def test_c4_segment_clean_on_device(big):
     """C4: the whole 100,352-set segment, inputs resident in HBM: every block valid
-    in ONE batch check (no retry)"""
+    in ONE batch check (no retry), and six sampled blocks valid under the C
+    restatement (oracle/bls_ref.c) too"""
     import torch
     a = bench.build_segment(list(range(1024)))
     assert a["n_sets"] == 100352 and int(a["pk_offsets"][-1]) == 12978176
@@ -186,6 +187,11 @@ def test_c4_segment_clean_on_device(big):
     assert (jr == 1).all()
     st = big.last_stats
     assert st.batch_retries == 0 and st.batch_sigs_success == 100352 and st.pubkeys_aggregated == 12978176
+    # sampled blocks (first, middle, last, and three more) re-verified by the C
+    # restatement on the same keys, messages and device signatures
+    host = dict(a, sigs=sigs.cpu().numpy(), sig_len=np.full(a["n_sets"], 96, np.uint32))
+    pick = [0, 511, 1023] + [int(x) for x in np.random.default_rng(SEED).choice(np.arange(1, 1023), 3, replace=False)]
+    _cref_block_check(big, host, pick, np.ones(1024, np.int32))
 
 
 def test_c5_faulted_segment_host_resident(big):
