@@ -193,6 +193,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
             return _lib
         if not os.path.exists(path):
             raise BgvNativeError(BGV_E_NO_DEVICE, f"{path} not built (run __graft_entry__.build())")
+        # One HIP runtime per process: torch ships its own libamdhip64 with the
+        # same soname as /opt/rocm's.  Loaded first, torch's copy satisfies
+        # libbgv's dependency; loaded after libbgv, torch brings a second
+        # runtime that cannot open the GPU ("No HIP GPUs are available").
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         try:
             lib = ctypes.CDLL(path)
             build_id_fn = lib.bgv_build_id
