@@ -49,6 +49,8 @@ def build(force=False, verbose=False, lib=LIB, defines=()):
         o = os.path.join(CSRC, os.path.basename(lib) + "." + s.replace(".hip", ".o"))
         cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
                "-I" + os.path.join(ROOT, "include")] + ["-D" + x for x in defines] + [f'-DBGV_SRC_HASH="{bid}"', "-c", os.path.join(CSRC, s), "-o", o]
+        if defines and os.environ.get("BGV_VARIANT_FLAGS"):  # variant builds only (A/B experiments)
+            cmd[1:1] = os.environ["BGV_VARIANT_FLAGS"].split()
         if verbose:
             print(" ".join(cmd), flush=True)
         procs.append(subprocess.Popen(cmd))

@@ -18,7 +18,9 @@ def main():
     ap.add_argument("--ctx", type=int, default=2)
     ap.add_argument("--steps", type=int, default=8, help="batches per context")
     ap.add_argument("--blocks", type=int, default=1024)
+    ap.add_argument("--cfg", action="append", default=[], metavar="KEY=VAL", help="bgv_cfg override for every context")
     args = ap.parse_args()
+    cfg = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in args.cfg}
     import numpy as np
     import torch
 
@@ -29,7 +31,7 @@ def main():
     seg = bench.build_segment(list(range(args.blocks)))
     ctxs, arrs = [], []
     for k in range(args.ctx):
-        d = native.Device(0)
+        d = native.Device(0, **cfg)
         d.gen_keys(0, bench.N_VALIDATORS, bench.SEED)
         da = bench.to_device(seg, torch, dev)
         sigs = torch.zeros((seg["n_sets"], 192), dtype=torch.uint8, device=dev)
@@ -62,7 +64,8 @@ def main():
         t.join()
     par = (time.perf_counter() - t0) / (args.steps * args.ctx) * 1e3
     print(json.dumps({"mode": f"{args.ctx} contexts in flight", "ms_per_batch": round(par, 3), "ok": all(oks),
-                      "gain": round(seq / par, 4), "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")}), flush=True)
+                      "gain": round(seq / par, 4), "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                      **({"cfg": cfg} if cfg else {})}), flush=True)
     for d in ctxs:
         d.close()
 
