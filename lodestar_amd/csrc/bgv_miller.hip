@@ -131,8 +131,11 @@ void launch_miller_duo(hipStream_t st, const dev_batch& b, const dev_work& w) {
 // them at three times the per-iteration work.
 __global__ void __launch_bounds__(64, 1) k_miller_quad(dev_batch b, dev_work w, uint32_t count) {
   __shared__ quad_x_t sx[16];
+  __shared__ fp2_t zs;  // the zero operand (miller_quad.h address selects)
   const uint32_t lane = threadIdx.x, pr = lane >> 2, h = (lane >> 1) & 1u, s = lane & 1u;
   const uint32_t t = blockIdx.x * 16u + pr;
+  zs = fp2_zero();  // every lane stores the same value; the wave's first read follows it in issue order
+  coop_wave_sync();
   if (t >= count) return;  // the four lanes of a pair leave together
   if (w.pk_code[t] != C_OK) {  // rejected job: its Miller values are never used
     if (s == 0) {
@@ -147,7 +150,7 @@ __global__ void __launch_bounds__(64, 1) k_miller_quad(dev_batch b, dev_work w, 
   const g1a P = w.rpk_aff[t];
   const g2a Q = w.h_aff[t];
   fp6_t fh;
-  quad_miller(fh, P, Q, h, s, sx[pr]);
+  quad_miller(fh, P, Q, h, s, sx[pr], &zs);
   if (s == 0) {
     if (h) w.f_set[t].c1 = fh;
     else w.f_set[t].c0 = fh;

@@ -28,7 +28,7 @@ struct quad_x_t {
   fp2_t F[6];   // published f halves (F[3h + k]); in the S recombination the Fp6 values u / t; in L, F0 / F1
   fp2_t R[16];  // product exchange: R[4 rho + round]
   fp2_t L[4];   // line a0, a1, b1, a1 + b1
-};                // 26 Fp2 = 2,496 B per pair: 4 waves (64 pairs) per CU
+};                // 26 Fp2 = 2,496 B per pair (+ one zero slot per block): 4 waves (64 pairs) per CU
 
 __device__ __forceinline__ fp2_t q_sel4(uint32_t r, const fp2_t& a, const fp2_t& b, const fp2_t& c, const fp2_t& d) {
   fp2_t x, y, z;
@@ -52,24 +52,35 @@ __device__ __forceinline__ fp2_t q_lazy(const fp2_t& a, const fp2_t& b) {  // < 
 BGV_CONST uint8_t QUAD_PI[3] = {0, 0, 1};
 BGV_CONST uint8_t QUAD_PJ[3] = {1, 2, 2};
 
-// S-round operand X(m) of half h: f0[m] + f1[m] (h = 0, a = f0 + f1) or f0[m] (h = 1)
-__device__ __forceinline__ fp2_t quad_sx(const quad_x_t& X, uint32_t h, uint32_t m) {
-  const fp2_t f0 = X.F[m];
-  const fp2_t f1 = X.F[3 + m];
-  const fp2_t z = q_sel2(h != 0, fp2_zero(), f1);
+// Operands that are conditionally zero are read through a lane-selected LDS
+// address, the per-block zero slot zp standing for 0 (one address select
+// instead of a 24-dword value select per operand; BGV_QUAD_ZSLOT 0: value select)
+#ifndef BGV_QUAD_ZSLOT
+#define BGV_QUAD_ZSLOT 1
+#endif
+#if BGV_QUAD_ZSLOT
+#define QUAD_OR_ZERO(c, p) (*((c) ? (p) : zp))
+#else
+#define QUAD_OR_ZERO(c, p) q_sel2((c), *(p), fp2_zero())
+#endif
+// S-round operand X(m) of half h: f0[m] + f1[m] (h = 0, a = f0 + f1) or f0[m]
+// (h = 1); 0 when `zero` (sub-lane 0's unpaired second operand)
+__device__ __forceinline__ fp2_t quad_sx(const quad_x_t& X, uint32_t h, uint32_t m, const fp2_t* zp, bool zero) {
+  const fp2_t f0 = QUAD_OR_ZERO(!zero, &X.F[m]);
+  const fp2_t f1 = QUAD_OR_ZERO(!zero && !h, &X.F[3 + m]);
   fp2_t r;
-  fp2_add(r, f0, z);
+  fp2_add(r, f0, f1);
   return r;
 }
 // S-round operand Y(m): f0[m] + (v f1)[m] (h = 0, b = f0 + v f1) or f1[m] (h = 1);
-// (v f1) = (xi f1[2], f1[0], f1[1])
-__device__ __forceinline__ fp2_t quad_sy(const quad_x_t& X, uint32_t h, uint32_t m) {
+// (v f1) = (xi f1[2], f1[0], f1[1]); 0 when `zero`
+__device__ __forceinline__ fp2_t quad_sy(const quad_x_t& X, uint32_t h, uint32_t m, const fp2_t* zp, bool zero) {
   const uint32_t i1 = h ? m : (m + 2u) % 3u;
-  fp2_t g = X.F[3 + i1];
+  fp2_t g = QUAD_OR_ZERO(!zero, &X.F[3 + i1]);
   fp2_t gx;
   fp2_mul_xi(gx, g);
   g = q_sel2(!h && m == 0, gx, g);
-  const fp2_t f0 = q_sel2(h != 0, fp2_zero(), X.F[m]);
+  const fp2_t f0 = QUAD_OR_ZERO(!zero && !h, &X.F[m]);
   fp2_t r;
   fp2_add(r, f0, g);
   return r;
@@ -132,7 +143,7 @@ __device__ __forceinline__ void quad_dbl_tail(g2p_t& T, const fp2_t& x2, const f
 // published to X.F, and the doubling tail.  fh is this lane's half of f
 // (consumed); leaves this lane's half of f^2 in fh.
 __device__ __forceinline__ void quad_sqr_dbl(fp6_t& fh, g2p_t& T, const fp2_t& x2, const fp_t& xp, const fp_t& yp,
-                                             uint32_t h, uint32_t s, uint32_t rho, quad_x_t& X) {
+                                             uint32_t h, uint32_t s, uint32_t rho, quad_x_t& X, const fp2_t* zp) {
   if (s == 0) {
     X.F[3 * h] = fh.c0;
     X.F[3 * h + 1] = fh.c1;
@@ -142,10 +153,8 @@ __device__ __forceinline__ void quad_sqr_dbl(fp6_t& fh, g2p_t& T, const fp2_t& x
 #pragma unroll 1
   for (uint32_t k = 0; k < 3; k++) {
     const uint32_t i = s ? QUAD_PI[k] : k, j = QUAD_PJ[k];
-    fp2_t xa = quad_sx(X, h, i), ya = quad_sy(X, h, i);
-    fp2_t xb = quad_sx(X, h, j), yb = quad_sy(X, h, j);
-    xb = q_sel2(s != 0, xb, fp2_zero());
-    yb = q_sel2(s != 0, yb, fp2_zero());
+    const fp2_t xa = quad_sx(X, h, i, zp, false), ya = quad_sy(X, h, i, zp, false);
+    const fp2_t xb = quad_sx(X, h, j, zp, s == 0), yb = quad_sy(X, h, j, zp, s == 0);
     fp2_t r;
     fp2_mul(r, q_lazy(xa, xb), q_lazy(ya, yb));
     X.R[4 * rho + k] = r;  // R is disjoint from F: no ordering hazard
@@ -191,13 +200,13 @@ __device__ __forceinline__ void quad_sqr_dbl(fp6_t& fh, g2p_t& T, const fp2_t& x
   o.c0 = X.F[3 * (h ^ 1u)];
   o.c1 = X.F[3 * (h ^ 1u) + 1];
   o.c2 = X.F[3 * (h ^ 1u) + 2];
-  fp6_t u, t, f0, f1, vt;
-  duo_sel6(u, h != 0, o, c);
-  duo_sel6(t, h != 0, c, o);
-  fp6_mul_v(vt, t);
-  fp6_sub(f0, u, t);
-  fp6_sub(f0, f0, vt);  // u - t - v t
-  fp6_add(f1, t, t);    // 2 t
+  // half 0 holds u (c) and reads t (o): f0 = u - t - v t; half 1 holds t: f1 = 2 t.
+  // Both formulas run on every lane on (c, o) and the lane keeps its own.
+  fp6_t f0, f1, vt;
+  fp6_mul_v(vt, o);
+  fp6_sub(f0, c, o);
+  fp6_sub(f0, f0, vt);  // u - t - v t (half 0)
+  fp6_add(f1, c, c);    // 2 t (half 1)
   duo_sel6(fh, h != 0, f1, f0);
 }
 
@@ -216,7 +225,7 @@ BGV_CONST quad_op QUAD_L[4][4] = {
 // f <- f * (a0 + a1 v + b1 v w) with the line in X.L; this lane's half of f
 // in fh.  The spare slot of lane 2 squares T.x: x2 = X^2 of the new T.
 __device__ __forceinline__ void quad_line(fp6_t& fh, fp2_t& x2, const g2p_t& T, uint32_t h, uint32_t s, uint32_t rho,
-                                          quad_x_t& X) {
+                                          quad_x_t& X, const fp2_t* zp) {
   // publish F0 / F1 (X.F is free: every lane has read the u / t values)
   coop_wave_sync();
   if (s == 0) {
@@ -237,14 +246,13 @@ __device__ __forceinline__ void quad_line(fp6_t& fh, fp2_t& x2, const g2p_t& T, 
     const quad_op e = QUAD_L[rho][r];
     fp2_t a, b;
     {
-      const fp2_t z = fp2_zero();
-      fp2_t x0 = q_sel2(e.w0 != 0, X.F[e.i], z), x1 = q_sel2(e.w1 != 0, X.F[3 + e.i], z);
-      fp2_t y0 = q_sel2(e.w0 != 0 && e.pair, X.F[e.j], z), y1 = q_sel2(e.w1 != 0 && e.pair, X.F[3 + e.j], z);
+      const fp2_t x0 = QUAD_OR_ZERO(e.w0 != 0, &X.F[e.i]), x1 = QUAD_OR_ZERO(e.w1 != 0, &X.F[3 + e.i]);
+      const fp2_t y0 = QUAD_OR_ZERO(e.w0 && e.pair, &X.F[e.j]), y1 = QUAD_OR_ZERO(e.w1 && e.pair, &X.F[3 + e.j]);
       fp2_t ai, aj;
       fp2_add(ai, x0, x1);
       fp2_add(aj, y0, y1);
       a = q_lazy(ai, aj);
-      const fp2_t l0 = X.L[e.li], l1 = q_sel2(e.lpair != 0, X.L[e.lj], z);
+      const fp2_t l0 = X.L[e.li], l1 = QUAD_OR_ZERO(e.lpair != 0, &X.L[e.lj]);
       b = q_lazy(l0, l1);
     }
     // rho 2, round 3: X^2 of the new T (for the next doubling step's 3X^2 xP)
@@ -354,7 +362,7 @@ __device__ __forceinline__ void quad_add(g2p_t& T, const g2a& Q, const fp_t& xp,
 
 // the pair (P, Q) on lanes 4k .. 4k+3: fh = this lane's half of f_{x,Q}(P)
 // for the negative x (conjugated)
-__device__ void quad_miller(fp6_t& fh, const g1a& P, const g2a& Q, uint32_t h, uint32_t s, quad_x_t& X) {
+__device__ void quad_miller(fp6_t& fh, const g1a& P, const g2a& Q, uint32_t h, uint32_t s, quad_x_t& X, const fp2_t* zp) {
   const uint32_t rho = 2 * h + s;
   g2p_t T;
   T.x = Q.x;
@@ -383,12 +391,12 @@ __device__ void quad_miller(fp6_t& fh, const g1a& P, const g2a& Q, uint32_t h, u
       duo_sel6(fh, h != 0, l1, l0);
       fp2_sqr(x2, T.x);
     } else {
-      quad_sqr_dbl(fh, T, x2, P.x, P.y, h, s, rho, X);
-      quad_line(fh, x2, T, h, s, rho, X);
+      quad_sqr_dbl(fh, T, x2, P.x, P.y, h, s, rho, X, zp);
+      quad_line(fh, x2, T, h, s, rho, X, zp);
     }
     if ((BLS_X_ABS >> bit) & 1ull) {
       quad_add(T, Q, P.x, P.y, rho, X);
-      quad_line(fh, x2, T, h, s, rho, X);
+      quad_line(fh, x2, T, h, s, rho, X, zp);
     }
   }
   if (h) fp6_neg(fh, fh);  // x < 0: conjugate (negate f1)
