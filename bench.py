@@ -417,7 +417,7 @@ def host_resident_c4(d, arrays_host: dict, reps: int = 3, ds=None):
     return out
 
 
-def shard_projection(d, torch, dev, arrays_host: dict, ds=None, worlds=(2, 4, 8), reps: int = 5):
+def shard_projection(d, torch, dev, arrays_host: dict, ds=None, worlds=(2, 4, 8), reps: int = 5, ds_small=None):
     """Strong sharding of ONE C4 segment measured on one GPU: each rank's
     shard (dist.shard_jobs) through bgv_partial, plus the node's combination of
     `world` partials (bgv_combine_final).  ms = median partial + combine; the
@@ -426,13 +426,15 @@ def shard_projection(d, torch, dev, arrays_host: dict, ds=None, worlds=(2, 4, 8)
     contexts of the batches in flight), ms_in_flight = the shard's time per
     segment with len(ds) segments in flight (dist.run_in_flight: partials on
     worker threads, combinations in order on this thread), the per-GPU pace of
-    a node verifying a stream of segments."""
+    a node verifying a stream of segments; shards under INFLIGHT_SMALL_BELOW
+    sets run with `ds_small` (INFLIGHT_SMALL contexts), the depth an N-rank
+    run of this bench uses for them."""
     from concurrent.futures import ThreadPoolExecutor
 
     from lodestar_amd.dist import batch_job_work, run_in_flight, select_jobs, shard_balance, shard_jobs
     work = batch_job_work(arrays_host)
     out = {}
-    ex = ThreadPoolExecutor(max_workers=len(ds)) if ds and len(ds) > 1 else None
+    ex = ThreadPoolExecutor(max_workers=max(len(ds), len(ds_small or ()))) if ds and len(ds) > 1 else None
     for world in worlds:
         shards = shard_jobs(work, world)
         # the heaviest shard sets the node's time
@@ -453,19 +455,21 @@ def shard_projection(d, torch, dev, arrays_host: dict, ds=None, worlds=(2, 4, 8)
              "work_max_over_mean": round(shard_balance(work, shards), 4),
              "projected_sets_per_s": round(arrays_host["n_sets"] / ms * 1e3, 1)}
         if ex is not None:
+            dd = ds_small if ds_small and sub["n_sets"] < INFLIGHT_SMALL_BELOW else ds
+
             def submit(k):
-                return ex.submit(ds[k % len(ds)].partial, sub, on_device=True)
+                return ex.submit(dd[k % len(dd)].partial, sub, on_device=True)
 
             def finish(k, res):
-                return ds[k % len(ds)].combine_final([res[0]] * world) and res[3]
+                return dd[k % len(dd)].combine_final([res[0]] * world) and res[3]
 
-            n = 4 * len(ds)
-            assert run_in_flight(submit, finish, len(ds), len(ds))
+            n = 4 * len(dd)
+            assert run_in_flight(submit, finish, len(dd), len(dd))
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-            assert run_in_flight(submit, finish, n, len(ds))
+            assert run_in_flight(submit, finish, n, len(dd))
             mi = (time.perf_counter() - t1) / n * 1e3
-            e.update(ms_in_flight=round(mi, 3), inflight=len(ds),
+            e.update(ms_in_flight=round(mi, 3), inflight=len(dd),
                      projected_sets_per_s_in_flight=round(arrays_host["n_sets"] / mi * 1e3, 1))
         out[f"c4_over_{world}"] = e
     if ex is not None:
@@ -736,10 +740,22 @@ def main():
         host["sig_len"] = np.full(n_sets, 96, np.uint32)
         host["scalars"] = None
         legs["c4_host_resident"] = host_resident_c4(d, host, ds=ds)
-        legs["c4_epoch_slice"] = epoch_slice(d, torch, dev, arrays, host["sigs"], ds=ds)
+        # batches under INFLIGHT_SMALL_BELOW sets go INFLIGHT_SMALL deep (as an
+        # N-rank run of this bench does with its shards)
+        ds_small = list(ds)
+        while len(ds_small) < INFLIGHT_SMALL:
+            x = native.Device(gpu, **cfg)
+            x.gen_keys(0, N_VALIDATORS, SEED)
+            ds_small.append(x)
+        legs["c4_epoch_slice"] = epoch_slice(d, torch, dev, arrays, host["sigs"], ds=ds_small)
         legs["mixed_sizes"] = mixed_sizes(d, darr)
         if world == 1:
-            legs["strong_shard_projection"] = shard_projection(d, torch, dev, host, ds)
+            legs["strong_shard_projection"] = shard_projection(d, torch, dev, host, ds, ds_small=ds_small)
+        # closed before the reserved-device leg opens its CU-masked streams (each
+        # takes a hardware queue of its own, with its own scratch)
+        for x in ds_small[len(ds):]:
+            x.close()
+        if world == 1:
             legs["reserved_device"] = reserved_device(d, gpu, torch, dev, darr, host)
 
     # roofline (INT32 VALU): algorithmic Fp-mul per set x sets / the stage's
