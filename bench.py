@@ -592,6 +592,9 @@ def main():
     ap.add_argument("--inflight", type=int, default=0,
                     help="batches in flight per GPU: contexts on the GPU, one worker thread each (dist.run_in_flight); "
                          "0 = auto (3, or 4 for batches under 32,000 sets per GPU)")
+    ap.add_argument("--input-sync", choices=("once", "per-call"), default="once",
+                    help="device inputs of the timed steps: synchronised once before them (default), or torch's "
+                         "stream waited for on every call")
     ap.add_argument("--cfg", action="append", default=[], metavar="KEY=VAL",
                     help="bgv_cfg override for every context (A/B runs only, e.g. pairs=4)")
     args = ap.parse_args()
@@ -668,12 +671,18 @@ def main():
     stage_sum = np.zeros(native.N_STAGES)
     t_sub, lat = {}, []
 
+    # the inputs are written once above and only read by the steps: one
+    # synchronisation here instead of a wait for torch's stream on every call
+    # (--input-sync per-call restores it)
+    torch.cuda.synchronize()
+    per_call = args.input_sync == "per-call"
+
     def submit(k):
         c = ds[k % len(ds)]
         t_sub[k] = time.perf_counter()
         if world == 1:
-            return ex.submit(c.verify, darr, on_device=True, want_set_codes=False)
-        return ex.submit(c.partial, darr, on_device=True)
+            return ex.submit(c.verify, darr, on_device=True, want_set_codes=False, sync_inputs=per_call)
+        return ex.submit(c.partial, darr, on_device=True, sync_inputs=per_call)
 
     def finish(k, res):
         c = ds[k % len(ds)]

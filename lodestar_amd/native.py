@@ -346,7 +346,12 @@ class Device:
 
     # --------------------------------------------------------------- batches
     @staticmethod
-    def make_batch(arrays: dict, on_device: bool = False) -> BgvBatch:
+    def make_batch(arrays: dict, on_device: bool = False, sync_inputs: bool = True) -> BgvBatch:
+        """sync_inputs=False: the caller guarantees device-resident inputs are
+        complete (e.g. one torch.cuda.synchronize() after they were written, for
+        inputs that are only read afterwards), and the per-call wait for torch's
+        current stream is skipped; that wait can sit behind other contexts'
+        kernels on a shared hardware queue."""
         b = BgvBatch()
         b.n_sets = int(arrays["n_sets"])
         b.n_jobs = int(arrays["n_jobs"])
@@ -360,23 +365,23 @@ class Device:
         b.sig_len = _ptr(arrays.get("sig_len"))
         b.scalars = _ptr(arrays.get("scalars"))
         b.on_device = 1 if on_device else 0
-        if on_device:
+        if on_device and sync_inputs:
             _sync_producers(arrays)
         return b
 
-    def verify(self, arrays: dict, on_device: bool = False, want_set_codes: bool = True):
+    def verify(self, arrays: dict, on_device: bool = False, want_set_codes: bool = True, sync_inputs: bool = True):
         """returns (job_result int32[n_jobs], set_code int32[n_sets] | None)"""
-        b = self.make_batch(arrays, on_device)
+        b = self.make_batch(arrays, on_device, sync_inputs)
         jr = np.zeros(max(b.n_jobs, 1), dtype=np.int32)
         sc = np.zeros(max(b.n_sets, 1), dtype=np.int32) if want_set_codes else None
         self._check(self.lib.bgv_verify(self.h, ctypes.byref(b), jr.ctypes.data,
                                         sc.ctypes.data if sc is not None else None, ctypes.byref(self.last_stats)))
         return jr[: b.n_jobs], (sc[: b.n_sets] if sc is not None else None)
 
-    def partial(self, arrays: dict, on_device: bool = False):
+    def partial(self, arrays: dict, on_device: bool = False, sync_inputs: bool = True):
         """bgv_partial: (miller576 bytes, set codes, provisional job results
         (-code rejected / 1 pending the combined check), no-job-rejected)."""
-        b = self.make_batch(arrays, on_device)
+        b = self.make_batch(arrays, on_device, sync_inputs)
         out = np.zeros(576, dtype=np.uint8)
         sc = np.zeros(max(b.n_sets, 1), dtype=np.int32)
         jr = np.zeros(max(b.n_jobs, 1), dtype=np.int32)
