@@ -417,7 +417,7 @@ def host_resident_c4(d, arrays_host: dict, reps: int = 3, ds=None):
     return out
 
 
-def shard_projection(d, torch, dev, arrays_host: dict, ds=None, worlds=(2, 4, 8), reps: int = 5, ds_small=None):
+def shard_projection(d, torch, dev, arrays_host: dict, ds=None, worlds=(2, 4, 8), reps: int = 5):
     """Strong sharding of ONE C4 segment measured on one GPU: each rank's
     shard (dist.shard_jobs) through bgv_partial, plus the node's combination of
     `world` partials (bgv_combine_final).  ms = median partial + combine; the
@@ -426,15 +426,14 @@ def shard_projection(d, torch, dev, arrays_host: dict, ds=None, worlds=(2, 4, 8)
     contexts of the batches in flight), ms_in_flight = the shard's time per
     segment with len(ds) segments in flight (dist.run_in_flight: partials on
     worker threads, combinations in order on this thread), the per-GPU pace of
-    a node verifying a stream of segments; shards under INFLIGHT_SMALL_BELOW
-    sets run with `ds_small` (INFLIGHT_SMALL contexts), the depth an N-rank
-    run of this bench uses for them."""
+    a node verifying a stream of segments (an N-rank run of this bench takes
+    shards under INFLIGHT_SMALL_BELOW sets INFLIGHT_SMALL deep)."""
     from concurrent.futures import ThreadPoolExecutor
 
     from lodestar_amd.dist import batch_job_work, run_in_flight, select_jobs, shard_balance, shard_jobs
     work = batch_job_work(arrays_host)
     out = {}
-    ex = ThreadPoolExecutor(max_workers=max(len(ds), len(ds_small or ()))) if ds and len(ds) > 1 else None
+    ex = ThreadPoolExecutor(max_workers=len(ds)) if ds and len(ds) > 1 else None
     for world in worlds:
         shards = shard_jobs(work, world)
         # the heaviest shard sets the node's time
@@ -455,7 +454,7 @@ def shard_projection(d, torch, dev, arrays_host: dict, ds=None, worlds=(2, 4, 8)
              "work_max_over_mean": round(shard_balance(work, shards), 4),
              "projected_sets_per_s": round(arrays_host["n_sets"] / ms * 1e3, 1)}
         if ex is not None:
-            dd = ds_small if ds_small and sub["n_sets"] < INFLIGHT_SMALL_BELOW else ds
+            dd = ds
 
             def submit(k):
                 return ex.submit(dd[k % len(dd)].partial, sub, on_device=True)
@@ -749,19 +748,14 @@ def main():
         host["sig_len"] = np.full(n_sets, 96, np.uint32)
         host["scalars"] = None
         legs["c4_host_resident"] = host_resident_c4(d, host, ds=ds)
-        # batches under INFLIGHT_SMALL_BELOW sets go INFLIGHT_SMALL deep (as an
-        # N-rank run of this bench does with its shards)
-        ds_small = list(ds)
-        while len(ds_small) < INFLIGHT_SMALL:
-            x = native.Device(gpu, **cfg)
-            x.gen_keys(0, N_VALIDATORS, SEED)
-            ds_small.append(x)
-        legs["c4_epoch_slice"] = epoch_slice(d, torch, dev, arrays, host["sigs"], ds=ds_small)
+        # (the legs below run len(ds) deep; an N-rank run takes its shards
+        # INFLIGHT_SMALL deep, profiles/r06o_depth_streams/: a fourth context
+        # here, open beside the reserved leg's CU-masked queues, coincided with
+        # queue scratch failures there)
+        legs["c4_epoch_slice"] = epoch_slice(d, torch, dev, arrays, host["sigs"], ds=ds)
         legs["mixed_sizes"] = mixed_sizes(d, darr)
         if world == 1:
-            legs["strong_shard_projection"] = shard_projection(d, torch, dev, host, ds, ds_small=ds_small)
-        for x in ds_small[len(ds):]:
-            x.close()
+            legs["strong_shard_projection"] = shard_projection(d, torch, dev, host, ds)
 
     # roofline (INT32 VALU): algorithmic Fp-mul per set x sets / the stage's
     # HIP-event time in the timed steps, for every stage; the dominant kernel
