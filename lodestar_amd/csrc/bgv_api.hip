@@ -12,6 +12,7 @@
 #include <stdio.h>
 #include <stdarg.h>
 #include <stdlib.h>
+#include <atomic>
 #include <vector>
 #include <string>
 
@@ -67,6 +68,7 @@ struct bgv_ctx {
   int run_from = 0, run_to = 0;  // stage range of the last run_stages (bgv_last_stats)
   dev_batch last_d = {};         // the last run_stages batch (its pipeline variant for bgv_stats)
   hipStream_t st = nullptr, st_hash = nullptr, st_pk = nullptr;
+  bool busy = false;  // prepare(): another batch of this process was in flight on the device
   hipStream_t st_chk = nullptr;  // deferred subgroup checks, low priority (BGV_CHK_STREAM)
   hipEvent_t ev[ST_COUNT + 1] = {};   // ev[s] = start of stage s on its stream
   hipEvent_t ev_end[ST_COUNT] = {};   // end of stage s on its stream
@@ -471,7 +473,22 @@ static int stage_issue(bgv_ctx* c, size_t total) {
 // latency mode by batch size (prepare(); the r02 sweep: 25,088 sets 24.5 ms
 // split against 26.3 ms, 50,176: 35.4 against 29.3; r03: to 65,536)
 static const uint32_t SPLIT_MAX = 59000;
-static bool layout_split(const bgv_cfg& k, uint32_t n) { return k.split >= 0 ? k.split != 0 : n < SPLIT_MAX; }
+// With other batches in flight on the device (this process's bgv_verify /
+// bgv_partial calls between entry and results), batches from INFLIGHT_BULK_MIN
+// sets take the bulk pipeline (one lane per set, two pairs per Miller item over
+// lines), whose kernels do the most work per instruction: with three in flight
+// 50,176 sets 19.7-19.8 -> 18.5-18.8 ms per batch, 37,632 sets 15.8-16.4 ->
+// 14.8-15.1 (profiles/r06ag_c4_over_2/); alone it loses (23.3-23.8 -> 29.1-29.8).
+static const uint32_t INFLIGHT_BULK_MIN = 32000;
+static std::atomic<int> g_active[64];
+struct active_guard {
+  int dev;
+  explicit active_guard(int d) : dev(d >= 0 && d < 64 ? d : -1) { if (dev >= 0) g_active[dev]++; }
+  ~active_guard() { if (dev >= 0) g_active[dev]--; }
+};
+static bool layout_split(const bgv_cfg& k, uint32_t n, bool busy) {
+  return k.split >= 0 ? k.split != 0 : (n < SPLIT_MAX && !(busy && n >= INFLIGHT_BULK_MIN));
+}
 
 // The hash maps of a latency-mode batch read only the messages, and they head
 // the critical path (maps -> clearing -> Miller -> fold -> final exp): they are
@@ -489,7 +506,7 @@ static int early_maps(bgv_ctx* c, dev_batch& d, bool after_staging) {
   const uint32_t n = d.n_sets;
   if (!BGV_EARLY_MAPS) return 0;
   const bool timed = c->cfg.timing >= 0 ? c->cfg.timing != 0 : n >= 65536;
-  if (!n || timed || !layout_split(c->cfg, n)) return 0;
+  if (!n || timed || !layout_split(c->cfg, n, c->busy)) return 0;
   if (int r = ensure_or_release_lines(c, c->q_part, 2 * (size_t)n)) return r;
   if (after_staging) HIPCHK(hipStreamWaitEvent(c->st_hash, c->ev_staged, 0));
   dev_work w;
@@ -517,6 +534,8 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
   if (b->n_raw && !b->raw_pks) return fail(BGV_E_INVALID_ARG, "n_raw > 0 but raw_pks is NULL");
   const uint32_t n = b->n_sets, J = b->n_jobs;
   memset(&d, 0, sizeof d);
+  // another batch of this process in flight on the device (read once per batch)
+  c->busy = c->device >= 0 && c->device < 64 && g_active[c->device].load() >= 2;
   d.n_sets = n;
   d.n_jobs = J;
   d.n_raw = b->n_raw;
@@ -615,8 +634,8 @@ static int prepare(bgv_ctx* c, const bgv_batch* b, dev_batch& d, bool need_sigs)
                         MSM_MIN = 6000, MSM4_MIN = 9000, MSM2_MIN = 32000, PAIRS2_MIN = 65536,
                         CLEAR3_MIN = 9000, KV6_MIN = 1100, KV3_MIN = 4500, KV_MAX = 11500;
   const bgv_cfg& k = c->cfg;
-  d.pairs_per_item = k.pairs ? (uint32_t)k.pairs : (n >= PAIRS2_MIN ? 2u : 1u);
-  d.split = layout_split(k, n) ? 1u : 0u;
+  d.pairs_per_item = k.pairs ? (uint32_t)k.pairs : (n >= PAIRS2_MIN || (c->busy && n >= INFLIGHT_BULK_MIN) ? 2u : 1u);
+  d.split = layout_split(k, n, c->busy) ? 1u : 0u;
   // one lane per point from 16,500 sets (25,088: 16.74 -> 16.5 ms; 17,248:
   // 14.24 -> 13.95 ms; the trio's waves oversubscribe the SIMDs there) and the
   // two-lane Miller loop from 15,000 (r04 sweep, profiles/r04z_sweep_cliff.txt:
@@ -952,6 +971,7 @@ int bgv_verify(bgv_ctx* c, const bgv_batch* b, int32_t* job_result, int32_t* set
   if (!c || !b || (!job_result && b->n_jobs)) return fail(BGV_E_INVALID_ARG, "null argument");
   c->partial_pending = false;
   HIPCHK(hipSetDevice(c->device));
+  active_guard ag(c->device);
   dev_batch d;
   if (int r = prepare(c, b, d, true)) return r;
   dev_work w;
@@ -983,6 +1003,7 @@ int bgv_partial(bgv_ctx* c, const bgv_batch* b, uint8_t* miller576, int32_t* set
   if (!c || !b || !miller576) return fail(BGV_E_INVALID_ARG, "null argument");
   c->partial_pending = false;
   HIPCHK(hipSetDevice(c->device));
+  active_guard ag(c->device);
   dev_batch d;
   if (int r = prepare(c, b, d, true)) return r;
   dev_work w;
